@@ -1,0 +1,132 @@
+/* rsl.h — C ABI of the MI355X-native radar signal chain (librsl.so, gfx950 / CDNA4).
+ *
+ * Drop-in boundary for the per-frame chain of zaidcontractor/radar-slam (snapshot 2025-11-21).
+ * The reference is pure Python with no FFI; its boundary is the Python class surface listed per
+ * entry point below (file:line in the reference tree).  The Python host layer
+ * radar-slam_amd/src/... keeps those module paths and signatures and binds these symbols with
+ * ctypes (radar-slam_amd/rsl/_lib.py; binding stubs for other hosts: INTEGRATION.md).
+ *
+ * Conventions
+ *   - every pointer named dev_* / void* data argument is DEVICE memory (hipMalloc / torch tensor);
+ *     complex values are interleaved float32 (c64) unless the name says c128 / f64;
+ *   - all launches are asynchronous on the handle's stream (rsl_set_stream); rsl_sync waits;
+ *   - return 0 (RSL_OK) or an RSL_ERR_* code; rsl_last_error(h) describes the last failure;
+ *   - one handle per (device, stream); handles share no mutable state.
+ */
+#ifndef RSL_H
+#define RSL_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSL_OK 0
+#define RSL_ERR_INVALID 1     /* bad argument (shape, null pointer)        -> Python ValueError   */
+#define RSL_ERR_UNSUPPORTED 2 /* FFT size / antenna count not implemented  -> Python ValueError   */
+#define RSL_ERR_HIP 3         /* HIP runtime error                          -> Python RuntimeError */
+
+#define RSL_METHOD_BEAMFORMING 0
+#define RSL_METHOD_MUSIC 1
+
+/* kernel ids for rsl_timing_read */
+#define RSL_K_RANGE_FFT 0
+#define RSL_K_DOPPLER_FFT 1
+#define RSL_K_DETECT 2
+#define RSL_K_OFFSETS 3
+#define RSL_K_EMIT 4
+#define RSL_K_DOA_SCAN 5
+#define RSL_K_CELL_EXTRAS 6
+#define RSL_K_CONFIDENCE 7
+#define RSL_K_VELOCITY 8
+#define RSL_K_COUNT 9
+
+typedef struct rsl_context* rsl_handle;
+
+int rsl_version(void);
+int rsl_create(rsl_handle* out, int device);
+int rsl_destroy(rsl_handle h);
+const char* rsl_last_error(rsl_handle h);
+int rsl_set_stream(rsl_handle h, void* hip_stream); /* NULL = null stream */
+int rsl_sync(rsl_handle h);
+int rsl_fft_supported(int n);
+
+/* Per-kernel device time (hipEvents recorded on the handle's stream around every launch). */
+int rsl_timing_enable(rsl_handle h, int on);
+int rsl_timing_reset(rsl_handle h);
+int rsl_timing_read(rsl_handle h, int kernel_id, double* total_ms, long long* launches);
+
+/* a7  SignalPreprocessor.generate_range_doppler_spectrum  (dechirp.py:168-213, incl. process_chirp
+ *     :143-166, dechirp_signal :122-141, apply_window :85-108, remove_dc :110-120, chirp_subset :183-187).
+ *     cube c64 [F, A, C_total, S]; chirps chirp0 .. chirp0+C-1 are used;
+ *     table c64 [S] = conj(reference_chirp) * window, built on the host in fp64 (dechirp.py:74-83);
+ *     dc_removal != 0 zeroes range bin 0 (== subtracting the complex mean before the FFT);
+ *     work c64 [F, A, C, S] scratch; rds c64 [F, A, S, C], fftshift on both axes. */
+int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
+            const void* table, int dc_removal, void* work, void* rds);
+
+/* a8  SignalPreprocessor.extract_range_doppler_peaks  (dechirp.py:215-278).
+ *     thr_power = 10^(threshold_db/10) - 1e-12 (a cell passes when (double)|rds|^2 > thr_power);
+ *     range gate i_lo <= range_bin <= i_hi (from linspace(0, rr*S, S) on the host);
+ *     mask u64 [F, A, S, W], W = ceil(C/64) (bit j%64 of word j/64 = peak at doppler j);
+ *     row_count i32 [F, A, S];  db_map f32 [F, A, S, C] (nullable) = 10 log10(|rds|^2 + 1e-12). */
+int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
+               void* mask, void* row_count, void* db_map);
+
+/* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
+ * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
+ *     entry_row_off i32 [F*A*S], cell_row_off i32 [F*S], scratch i32 [F*S],
+ *     entry_base i64 [F+1], cell_base i64 [F+1] (global exclusive offsets; [F] = totals),
+ *     frame_counts i64 [2F] (entries, cells per frame). */
+int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int F, int A, int S, int C,
+                     void* entry_row_off, void* cell_row_off, void* scratch, void* entry_base, void* cell_base,
+                     void* frame_counts);
+
+/* Emit the peak entries (e_* arrays, i32; e_pdb f64 = per-entry power_db, nullable) and the unique cells
+ * (c_frame i32, c_rc i32 = range_bin*C + doppler_bin, c_amask u32 = antennas with a peak there).
+ * e_cell maps each entry to its cell.  Items beyond *_cap are dropped (compare the totals). */
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A, int S, int C,
+                  const void* entry_row_off, const void* cell_row_off, const void* entry_base, const void* cell_base,
+                  long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin, void* e_dbin, void* e_cell,
+                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
+
+/* Host helper: MFMA operand layout of a steering table.  steer_c128 is the host [G][M] complex128
+ * matrix of AngleEstimator.generate_steering_vector (angle_estimation.py:92-107) over the azimuth grid
+ * (angle_estimation.py:59-60).  rsl_steer_table_floats returns the float count; *ntiles out. */
+long long rsl_steer_table_floats(int G, int M);
+int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_out, int* ntiles);
+
+/* a11-a16  extract_spatial_signature + music_spectrum / estimate_angle_music / estimate_angle_beamforming
+ *     (angle_estimation.py:67-176, 227-251; robust_angle_estimation.py:236-245).
+ *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = *ncell_dev if non-null else ncell.
+ *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
+ *     at the argmax (unit-norm s); out_spec f32 [n, G] (nullable) = MUSIC 1/(M-|a^H s|^2) with the
+ *     reference's den > 1e-12 rule, or the beamforming |a^H s|^2. */
+int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+            const void* ncell_dev, long long ncell, const void* steer_tab, int G, int method, void* out_idx,
+            void* out_gmax, void* out_spec);
+
+/* a11, a15, a26  normalised signature (c64 [n, A], nullable), ESPRIT closed form (f64 deg, nullable;
+ *     angle_estimation.py:178-225 with esprit_scale = lambda / (2 pi d)), spatial phase
+ *     angle(s1 conj(s0)) (f64, nullable; velocity_solver.py:136), az_out = az_table[gidx] (f64, nullable). */
+int rsl_cell_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                    const void* ncell_dev, long long ncell, double esprit_scale, const void* gidx,
+                    const void* az_table, void* sig_out, void* esprit_deg, void* phase, void* az_out);
+
+/* a19  RobustAngleEstimator.compute_angle_confidence (robust_angle_estimation.py:88-138) for n
+ *     (cell, grid index) pairs.  steer_c128 f64 [G][M][2] and steer_phase f64 [G][M] = np.angle(a) are
+ *     device copies of the host fp64 tables.  conf f64 [n]. */
+int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                   long long n, const void* gidx, const void* steer_c128, const void* steer_phase, void* conf);
+
+/* a25-a29  VelocitySolver.two_step_optimization / solve_velocity (velocity_solver.py:65-355): exact
+ *     box-constrained LS for (v_x, v_y) per segment (segments = frames).  az f64 [N] radians, y f64 [N]
+ *     observed phase, amask u32 [N] (nullable; multiplicity = popcount), seg i64 [F+1],
+ *     k = 4 pi dt / lambda, ridge >= 0, bounds4 (host) = {vx_lo, vx_hi, vy_lo, vy_hi};
+ *     out f64 [F, 8] = {vx, vy, cost, rmse, max_residual, n, det, 0}; resid/pred f64 [N] nullable. */
+int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask, const void* seg, int F, double k,
+                 double ridge, const double* bounds4, void* out, void* resid, void* pred);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSL_H */

@@ -1,0 +1,473 @@
+"""CPU oracle for the radar-slam per-frame signal chain — TEST INFRASTRUCTURE ONLY.
+
+This module is a NumPy/SciPy restatement of the reference algorithms of
+zaidcontractor/radar-slam (snapshot 2025-11-21).  It exists for two purposes only:
+
+  * the parity checker used by ``tests/``, ``__graft_entry__.smoke()``;
+  * the ``cpu_baseline`` leg of ``bench.py`` (kind "port").
+
+The product path (``radar-slam_amd/``) never imports it.  Every function cites the
+reference file:line it restates.  All arithmetic is float64 / complex128, exactly like
+the reference (numpy 2.2 pocketfft, scipy 1.15 LAPACK / ndimage).
+
+Parity pinning: ``tests/test_oracle_golden.py`` checks every function here against the
+golden vectors in ``tests/golden/`` that ``tests/golden/gen_golden.py`` produced by
+importing and running the reference itself in the build container.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+C_LIGHT = 3e8  # dechirp.py:61, angle_estimation.py:48, simulate_raw.py:70
+
+
+# ----------------------------------------------------------------------------------------
+# L0: synthetic FMCW cube (scripts/simulate_raw.py)
+# ----------------------------------------------------------------------------------------
+def synthesize_frame(scatterers: Sequence[Dict], *, fc=77e9, bandwidth=1e9, chirp_duration=40e-6,
+                     pri=100e-6, num_chirps=64, num_antennas=8, antenna_spacing=None,
+                     sampling_rate=10e6, noise_power=0.01, rng=None) -> np.ndarray:
+    """Restates ``FMCWRadarSimulator.synthesize_frame`` (simulate_raw.py:147-221).
+
+    ``scatterers`` is a list of dicts with keys range_sc, azimuth_sc, rcs, vr
+    (simulate_raw.py:174-178).  Noise comes from the global ``np.random`` legacy stream
+    (simulate_raw.py:216-218) unless ``rng`` (a ``np.random.RandomState``) is given; with
+    the same seed the output is bit-identical to the reference.
+    """
+    lam = C_LIGHT / fc
+    d = antenna_spacing or (lam / 2)
+    S = int(chirp_duration * sampling_rate)                     # simulate_raw.py:75
+    k_rate = bandwidth / chirp_duration                         # simulate_raw.py:76
+    pos = np.arange(num_antennas) * d                           # simulate_raw.py:79
+    sig = np.zeros((num_antennas, num_chirps, S), dtype=complex)
+    t = np.linspace(0, chirp_duration, S)                       # simulate_raw.py:165
+
+    def chirp(tt):                                              # simulate_raw.py:88-100
+        return np.exp(1j * (2 * np.pi * (fc * tt + 0.5 * k_rate * tt ** 2)))
+
+    ref = chirp(t)
+    for sc in scatterers:
+        r = sc.get('range_sc', 0.0)
+        az = sc.get('azimuth_sc', 0.0)
+        rcs = sc.get('rcs', -10.0)
+        vr = sc.get('vr', 0.0)
+        if r <= 0 or not np.isfinite([r, az, rcs, vr]).all():   # simulate_raw.py:181
+            continue
+        delay = 2 * r / C_LIGHT                                 # simulate_raw.py:122
+        amp = np.sqrt(10 ** (rcs / 10)) / (4 * np.pi * r ** 2)  # simulate_raw.py:125-126
+        dph = 4 * np.pi * vr * fc / C_LIGHT                     # simulate_raw.py:129
+        aph = np.zeros(num_antennas, dtype=complex)
+        for i in range(num_antennas):                           # simulate_raw.py:140-143
+            aph[i] = amp * np.exp(1j * (dph + 2 * np.pi * pos[i] * np.sin(az) / lam))
+        td = t - delay
+        valid = (td >= 0) & (td <= chirp_duration)
+        if np.any(valid):
+            bb = chirp(td[valid]) * np.conj(ref[valid])         # simulate_raw.py:201-204
+            # same per-element op order as the (chirp, antenna) loop at :190-209
+            sig[:, :, valid] += aph[:, None, None] * bb[None, None, :]
+    rs = rng if rng is not None else np.random
+    noise = np.sqrt(noise_power) * (rs.randn(*sig.shape) + 1j * rs.randn(*sig.shape))
+    sig += noise
+    return sig
+
+
+TEST_SCENE = [  # tests/test_synth_raw.py:165-190
+    {'range_sc': 20.0, 'azimuth_sc': 0.0, 'rcs': -10.0, 'vr': 0.0},
+    {'range_sc': 40.0, 'azimuth_sc': float(np.radians(45.0)), 'rcs': -8.0, 'vr': 5.0},
+    {'range_sc': 60.0, 'azimuth_sc': float(np.radians(-30.0)), 'rcs': -12.0, 'vr': -3.0},
+]
+
+
+# ----------------------------------------------------------------------------------------
+# L1: dechirp -> window -> DC -> 2-D FFT -> fftshift ; peaks (src/radar_signal/dechirp.py)
+# ----------------------------------------------------------------------------------------
+def reference_chirp(fc, bandwidth, chirp_duration, sampling_rate):
+    """dechirp.py:74-83 (t = linspace inclusive; phase in float64)."""
+    S = int(chirp_duration * sampling_rate)
+    t = np.linspace(0, chirp_duration, S)
+    k_rate = bandwidth / chirp_duration
+    return np.exp(1j * (2 * np.pi * (fc * t + 0.5 * k_rate * t ** 2)))
+
+
+def window(kind: str, n: int) -> np.ndarray:
+    """dechirp.py:99-106 (scipy.signal.windows, sym=True)."""
+    from scipy.signal import windows
+    if kind == 'hann':
+        return windows.hann(n)
+    if kind == 'hamming':
+        return windows.hamming(n)
+    if kind == 'blackman':
+        return windows.blackman(n)
+    raise ValueError(f"Unknown window type: {kind}")
+
+
+def range_doppler_spectrum(frame: np.ndarray, *, fc=77e9, bandwidth=1e9, chirp_duration=40e-6,
+                           sampling_rate=10e6, window_type='hann', dc_removal=True,
+                           chirp_subset=None) -> np.ndarray:
+    """Vectorised restatement of ``generate_range_doppler_spectrum`` (dechirp.py:168-213).
+
+    frame c128[A, C, S] -> rds c128[A, S, C]; fftshift on both axes (dechirp.py:211).
+    Bit-identical to the per-chirp loop (checked in tests against the reference).
+    """
+    if chirp_subset is not None:                                # dechirp.py:184-187
+        frame = frame[:, chirp_subset[0]:chirp_subset[1], :]
+    ref = reference_chirp(fc, bandwidth, chirp_duration, sampling_rate)
+    bb = frame * np.conj(ref)                                   # dechirp.py:139
+    bb = bb * window(window_type, frame.shape[-1])              # dechirp.py:108
+    if dc_removal:
+        bb = bb - np.mean(bb, axis=-1, keepdims=True)           # dechirp.py:120
+    rds = np.ascontiguousarray(np.transpose(bb, (0, 2, 1)))    # dechirp.py:193,205
+    rds = np.fft.fft2(rds, axes=(1, 2))                         # dechirp.py:208
+    return np.fft.fftshift(rds, axes=(1, 2))                    # dechirp.py:211
+
+
+def range_doppler_spectrum_loop(frame, **kw):
+    """Loop-faithful variant (per chirp, dechirp.py:196-205) used as the CPU baseline."""
+    chirp_subset = kw.pop('chirp_subset', None)
+    if chirp_subset is not None:
+        frame = frame[:, chirp_subset[0]:chirp_subset[1], :]
+    fc = kw.get('fc', 77e9)
+    ref = reference_chirp(fc, kw.get('bandwidth', 1e9), kw.get('chirp_duration', 40e-6),
+                          kw.get('sampling_rate', 10e6))
+    A, C, S = frame.shape
+    w = window(kw.get('window_type', 'hann'), S)
+    rds = np.zeros((A, S, C), dtype=complex)
+    for a in range(A):
+        for c in range(C):
+            b = frame[a, c, :] * np.conj(ref)
+            b = b * w
+            if kw.get('dc_removal', True):
+                b = b - np.mean(b)
+            rds[a, :, c] = b
+    return np.fft.fftshift(np.fft.fft2(rds, axes=(1, 2)), axes=(1, 2))
+
+
+def range_axis(bandwidth, S):
+    """dechirp.py:241 (range_resolution = c/2B, dechirp.py:67)."""
+    return np.linspace(0, (C_LIGHT / (2 * bandwidth)) * S, S)
+
+
+def doppler_axis(sampling_rate, C):
+    """dechirp.py:242 (labels use f_s, not the PRF)."""
+    return np.linspace(-sampling_rate / 2, sampling_rate / 2, C)
+
+
+def peak_mask(rds: np.ndarray, threshold_db=-20.0):
+    """Boolean peak mask of ``extract_range_doppler_peaks`` before the range gate
+    (dechirp.py:235-254): 3x3 maximum_filter (mode 'reflect') == db, and db > thr."""
+    from scipy.ndimage import maximum_filter
+    power_db = 10 * np.log10(np.abs(rds) ** 2 + 1e-12)         # dechirp.py:235-238
+    m = np.zeros(rds.shape, dtype=bool)
+    for a in range(rds.shape[0]):
+        sp = power_db[a]
+        m[a] = (maximum_filter(sp, size=3) == sp) & (sp > threshold_db)
+    return m, power_db
+
+
+def extract_peaks(rds: np.ndarray, *, bandwidth=1e9, sampling_rate=10e6, threshold_db=-20.0,
+                  min_range=1.0, max_range=200.0) -> Dict:
+    """Restates ``extract_range_doppler_peaks`` (dechirp.py:215-278) -> same dict."""
+    A, S, C = rds.shape
+    m, power_db = peak_mask(rds, threshold_db)
+    rng_m = range_axis(bandwidth, S)
+    dop = doppler_axis(sampling_rate, C)
+    peaks = []
+    for a in range(A):
+        ii, jj = np.where(m[a])                                 # dechirp.py:257 (C order)
+        for i, j in zip(ii, jj):
+            rv = rng_m[i]
+            if min_range <= rv <= max_range:                    # dechirp.py:263
+                peaks.append({'antenna': a, 'range_bin': i, 'doppler_bin': j, 'range_m': rv,
+                              'doppler_hz': dop[j], 'power_db': power_db[a, i, j]})
+    return {'peaks': peaks, 'range_bins_m': rng_m, 'doppler_bins_hz': dop,
+            'power_spectrum_db': power_db}
+
+
+def peak_arrays(rds: np.ndarray, **kw):
+    """Struct-of-arrays form of ``extract_peaks``: (antenna, range_bin, doppler_bin, power_db)."""
+    A, S, C = rds.shape
+    m, power_db = peak_mask(rds, kw.get('threshold_db', -20.0))
+    rng_m = range_axis(kw.get('bandwidth', 1e9), S)
+    gate = (rng_m >= kw.get('min_range', 1.0)) & (rng_m <= kw.get('max_range', 200.0))
+    m &= gate[None, :, None]
+    a, i, j = np.nonzero(m)
+    return a, i, j, power_db[a, i, j]
+
+
+# ----------------------------------------------------------------------------------------
+# L2: DoA (src/angle_estimation/angle_estimation.py, src/algorithms/robust_angle_estimation.py)
+# ----------------------------------------------------------------------------------------
+def azimuth_grid(search_range=(-90, 90), search_resolution=0.5):
+    """angle_estimation.py:59-60 / robust_angle_estimation.py:74-75."""
+    return np.arange(search_range[0], search_range[1] + search_resolution, search_resolution)
+
+
+def steering_vector(az_deg, num_antennas=8, fc=77e9, antenna_spacing=None):
+    """angle_estimation.py:92-107."""
+    lam = C_LIGHT / fc
+    d = antenna_spacing or lam / 2
+    pos = np.arange(num_antennas) * d
+    return np.exp(1j * (2 * np.pi * pos * np.sin(np.radians(az_deg)) / lam))
+
+
+def steering_matrix(grid_deg, num_antennas=8, fc=77e9, antenna_spacing=None):
+    """[G, M] matrix of ``steering_vector`` rows (same fp64 expression per element)."""
+    return np.stack([steering_vector(g, num_antennas, fc, antenna_spacing) for g in grid_deg])
+
+
+def spatial_signature(rds, r, d):
+    """angle_estimation.py:67-90."""
+    s = rds[:, r, d]
+    p = np.sum(np.abs(s) ** 2)
+    if p > 0:
+        s = s / np.sqrt(p)
+    return s
+
+
+def music_spectrum_eigh(sig, grid_deg, num_antennas=8, fc=77e9, antenna_spacing=None, num_sources=1):
+    """Loop-faithful ``music_spectrum`` (angle_estimation.py:109-154)."""
+    from scipy.linalg import eigh
+    R = np.outer(sig, sig.conj())
+    ev, V = eigh(R)
+    idx = np.argsort(ev)[::-1]
+    V = V[:, idx]
+    En = V[:, num_sources:]
+    out = np.zeros(len(grid_deg))
+    for i, az in enumerate(grid_deg):
+        a = steering_vector(az, num_antennas, fc, antenna_spacing)
+        den = np.abs(a.conj().T @ En @ En.conj().T @ a)
+        out[i] = 1.0 / den if den > 1e-12 else 0.0
+    return out
+
+
+def music_spectrum_closed(sigs, steer):
+    """Rank-1 closed form: den = M - |a^H s|^2 for unit-norm s.
+
+    sigs c128[N, M] (normalised), steer c128[G, M] -> f64[N, G].
+    Zero-power signature: reference En = identity columns e_{M-2..0} -> den = M-1.
+    """
+    M = steer.shape[1]
+    g = np.abs(sigs @ steer.conj().T) ** 2
+    den = M - g
+    zero = np.sum(np.abs(sigs) ** 2, axis=1) == 0
+    den[zero] = M - 1
+    return np.where(den > 1e-12, 1.0 / np.where(den > 1e-12, den, 1.0), 0.0)
+
+
+def beamforming_spectrum(sigs, steer):
+    """angle_estimation.py:239-245 vectorised: |a^H s|^2, f64[N, G]."""
+    return np.abs(sigs @ steer.conj().T) ** 2
+
+
+def esprit_svd(sig, fc=77e9, antenna_spacing=None, num_sources=1):
+    """Loop-faithful ``estimate_angle_esprit`` (angle_estimation.py:178-225)."""
+    from scipy.linalg import svd
+    lam = C_LIGHT / fc
+    d = antenna_spacing or lam / 2
+    try:
+        U, s, Vh = svd(np.column_stack([sig[:-1], sig[1:]]))
+        Us = U[:, :num_sources]
+        Phi = np.linalg.pinv(Us[:-1, :]) @ Us[1:, :]
+        ph = np.angle(np.linalg.eigvals(Phi)[0])
+        with np.errstate(invalid='ignore'):
+            return np.degrees(np.arcsin(ph * lam / (2 * np.pi * d)))
+    except Exception:
+        return 0.0
+
+
+def esprit_closed(sigs, fc=77e9, antenna_spacing=None):
+    """Closed form: principal eigvec v of X^H X (2x2), u = X v,
+    phi = u[:-1]^H u[1:] / u[:-1]^H u[:-1]; theta = asin(arg(phi) * lam / (2 pi d))."""
+    lam = C_LIGHT / fc
+    d = antenna_spacing or lam / 2
+    x0 = sigs[:, :-1]
+    x1 = sigs[:, 1:]
+    a = np.sum(np.abs(x0) ** 2, axis=1)
+    c = np.sum(np.abs(x1) ** 2, axis=1)
+    b = np.sum(np.conj(x0) * x1, axis=1)
+    lam1 = 0.5 * (a + c) + np.sqrt((0.5 * (a - c)) ** 2 + np.abs(b) ** 2)
+    use_first = a >= c
+    v0 = np.where(use_first, lam1 - c, b)
+    v1 = np.where(use_first, np.conj(b), lam1 - a)
+    u = v0[:, None] * x0 + v1[:, None] * x1
+    num = np.sum(np.conj(u[:, :-1]) * u[:, 1:], axis=1)
+    den = np.sum(np.abs(u[:, :-1]) ** 2, axis=1)
+    phi = np.where(den > 0, num / np.where(den > 0, den, 1.0), 0)
+    with np.errstate(invalid='ignore'):
+        return np.degrees(np.arcsin(np.angle(phi) * lam / (2 * np.pi * d)))
+
+
+def process_targets(rds, peak_info, method='music', *, fc=77e9, antenna_spacing=None,
+                    num_antennas=8, search_range=(-90, 90), search_resolution=0.5):
+    """Restates ``AngleEstimator.process_targets`` (angle_estimation.py:253-309) with the
+    closed forms (verified equal to eigh/svd in tests) -> list of target dicts."""
+    grid = azimuth_grid(search_range, search_resolution)
+    steer = steering_matrix(grid, num_antennas, fc, antenna_spacing)
+    out = []
+    if method not in ('music', 'esprit', 'beamforming'):
+        return out                                              # angle_estimation.py:286,304
+    for p in peak_info['peaks']:
+        s = spatial_signature(rds, p['range_bin'], p['doppler_bin'])
+        if method == 'music':
+            spec = music_spectrum_closed(s[None], steer)[0]
+            ang = grid[np.argmax(spec)]
+        elif method == 'esprit':
+            spec = None
+            ang = esprit_closed(s[None], fc, antenna_spacing)[0]
+        else:
+            spec = beamforming_spectrum(s[None], steer)[0]
+            ang = grid[np.argmax(spec)]
+        out.append({'range_m': p['range_m'], 'doppler_hz': p['doppler_hz'], 'power_db': p['power_db'],
+                    'azimuth_deg': ang, 'azimuth_rad': np.radians(ang), 'antenna': p['antenna'],
+                    'range_bin': p['range_bin'], 'doppler_bin': p['doppler_bin'],
+                    'spatial_signature': s, 'spectrum': spec})
+    return out
+
+
+def angle_confidence(sig, az_deg, num_antennas=8, fc=77e9, antenna_spacing=None):
+    """robust_angle_estimation.py:88-138."""
+    a = steering_vector(az_deg, num_antennas, fc, antenna_spacing)
+    corr = np.abs(a.conj().T @ sig)
+    sp = np.sum(np.abs(sig) ** 2)
+    nc = corr / np.sqrt(sp) if sp > 0 else 0.0
+    perr = np.mean(np.abs(np.angle(np.exp(1j * (np.angle(sig) - np.angle(a))))))
+    pc = np.exp(-perr)
+    pw = np.abs(sig) ** 2
+    nf = np.percentile(pw, 20)
+    if nf > 0:
+        snrc = min(1.0, np.log10(np.mean(pw) / nf) / 3.0)
+    else:
+        snrc = 0.0
+    return min(1.0, max(0.0, nc * 0.4 + pc * 0.3 + snrc * 0.3))
+
+
+class RobustOracle:
+    """Restates ``RobustAngleEstimator`` (robust_angle_estimation.py:23-436) with the
+    rank-1 interference analysis in closed form (num_sources = 1)."""
+
+    def __init__(self, fc=77e9, antenna_spacing=None, num_antennas=8, search_range=(-90, 90),
+                 search_resolution=1.0, temporal_window=5, confidence_threshold=0.7,
+                 smoothing_factor=0.3, max_targets=100):
+        from collections import deque
+        self._deque = deque
+        self.fc, self.M = fc, num_antennas
+        self.d = antenna_spacing
+        self.grid = azimuth_grid(search_range, search_resolution)
+        self.steer = steering_matrix(self.grid, num_antennas, fc, antenna_spacing)
+        self.W, self.thr, self.alpha, self.max_targets = (temporal_window, confidence_threshold,
+                                                          smoothing_factor, max_targets)
+        self.angle_history, self.confidence_history = {}, {}
+
+    def smooth(self, tid, ang, conf):                           # :274-330
+        if tid not in self.angle_history:
+            self.angle_history[tid] = self._deque(maxlen=self.W)
+            self.confidence_history[tid] = self._deque(maxlen=self.W)
+        self.angle_history[tid].append(ang)
+        self.confidence_history[tid].append(conf)
+        if len(self.angle_history[tid]) >= 2:
+            angs = np.array(self.angle_history[tid])
+            cs = np.array(self.confidence_history[tid])
+            w = cs / np.sum(cs) if np.sum(cs) > 0 else np.ones_like(cs) / len(cs)
+            r = np.radians(angs)
+            sm = np.degrees(np.arctan2(np.sum(w * np.sin(r)), np.sum(w * np.cos(r))))
+            prev = self.angle_history[tid][-2]
+            sm = self.alpha * sm + (1 - self.alpha) * prev
+            return sm, np.mean(cs)
+        return ang, conf
+
+    def process(self, rds, peak_info, frame_timestamp=None):    # :346-411
+        peaks = [p for p in peak_info['peaks'] if p['power_db'] > -25.0]
+        peaks.sort(key=lambda x: x['power_db'], reverse=True)
+        peaks = peaks[:self.max_targets]
+        out = []
+        for p in peaks:
+            s = spatial_signature(rds, p['range_bin'], p['doppler_bin'])
+            g = beamforming_spectrum(s[None], self.steer)[0]
+            ang0 = self.grid[np.argmax(g)]
+            conf0 = angle_confidence(s, ang0, self.M, self.fc, self.d)
+            tid = f"target_{p['range_bin']}_{p['doppler_bin']}"
+            ang, conf = self.smooth(tid, ang0, conf0)
+            if conf >= self.thr:
+                out.append({'range_m': p['range_m'], 'doppler_hz': p['doppler_hz'],
+                            'power_db': p['power_db'], 'azimuth_deg': ang,
+                            'azimuth_rad': np.radians(ang), 'confidence': conf, 'is_reliable': True,
+                            'antenna': p['antenna'], 'range_bin': p['range_bin'],
+                            'doppler_bin': p['doppler_bin'], 'spatial_signature': s,
+                            'target_id': tid, 'initial_angle': ang0})
+        return out
+
+
+# ----------------------------------------------------------------------------------------
+# L3: velocity (src/velocity_solver/velocity_solver.py)
+# ----------------------------------------------------------------------------------------
+def observed_phase(sigs):
+    """velocity_solver.py:136: angle(s[1] * conj(s[0]))."""
+    return np.angle(sigs[:, 1] * np.conj(sigs[:, 0]))
+
+
+def velocity_ls(az_rad, observed, *, lambda_c, dt=0.1, bounds=((-50, 50), (-50, 50)), ridge=0.0):
+    """Exact box-constrained LS for the identifiable (v_x, v_y) of the VelocitySolver cost
+    (velocity_solver.py:142-176, 178-307): with elevation 0 and p = r*d,
+    (w x p).d = 0 and d_z = 0, so cost = sum (y - k (vx cos az + vy sin az))^2,
+    k = 4 pi dt / lambda.  ``ridge`` adds ridge*(vx^2+vy^2) (velocity_solver_improved.py:261).
+    Returns (vx, vy, cost)."""
+    k = 4 * np.pi * dt / lambda_c
+    cz, sz = np.cos(az_rad), np.sin(az_rad)
+    y = np.asarray(observed, dtype=np.float64)
+    H = k * k * np.array([[cz @ cz, cz @ sz], [cz @ sz, sz @ sz]]) + ridge * np.eye(2)
+    b = k * np.array([cz @ y, sz @ y])
+
+    def cost(v):
+        r = y - k * (v[0] * cz + v[1] * sz)
+        return float(r @ r + ridge * (v[0] ** 2 + v[1] ** 2))
+
+    (lx, hx), (ly, hy) = bounds
+    cands = []
+    det = H[0, 0] * H[1, 1] - H[0, 1] ** 2
+    if det > 1e-300:
+        v = np.array([(H[1, 1] * b[0] - H[0, 1] * b[1]) / det, (H[0, 0] * b[1] - H[0, 1] * b[0]) / det])
+        if lx <= v[0] <= hx and ly <= v[1] <= hy:
+            return v[0], v[1], cost(v)
+    for fix, val in ((0, lx), (0, hx), (1, ly), (1, hy)):
+        o = 1 - fix
+        lo, hi = (lx, hx) if o == 0 else (ly, hy)
+        num = b[o] - H[o, fix] * val
+        x = num / H[o, o] if H[o, o] > 0 else 0.0
+        x = min(max(x, lo), hi)
+        v = np.zeros(2)
+        v[fix], v[o] = val, x
+        cands.append((cost(v), v))
+    c, v = min(cands, key=lambda t: t[0])
+    return v[0], v[1], c
+
+
+def solve_velocity_de(solver_cls_kwargs, targets, dt=0.1):
+    """Not used at runtime; documented pointer: the reference runs
+    scipy.optimize.differential_evolution (seed 42) at velocity_solver.py:218-263."""
+    raise NotImplementedError
+
+
+# ----------------------------------------------------------------------------------------
+# L4: pose integration (src/pose_integration/pose_integration.py)
+# ----------------------------------------------------------------------------------------
+def integrate_positions(vel, ts, p0=(0, 0, 0), method='trapezoidal', smoothing=True, window=5):
+    """pose_integration.py:67-111."""
+    N = len(vel)
+    dt = np.diff(ts)
+    pos = np.zeros((N, 3))
+    pos[0] = p0
+    for i in range(1, N):
+        if method == 'trapezoidal':
+            pos[i] = pos[i - 1] + 0.5 * dt[i - 1] * (vel[i - 1] + vel[i])
+        elif method == 'euler':
+            pos[i] = pos[i - 1] + dt[i - 1] * vel[i - 1]
+        else:
+            raise ValueError(f"Unknown integration method: {method}")
+    if smoothing and N > window:
+        from scipy.ndimage import uniform_filter1d
+        for i in range(3):
+            pos[:, i] = uniform_filter1d(pos[:, i], size=window, mode='nearest')
+    return pos

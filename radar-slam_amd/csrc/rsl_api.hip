@@ -1,0 +1,365 @@
+// rsl_api.hip — C-ABI layer of librsl.so (see include/rsl.h).  No kernels here: argument checks,
+// per-size twiddle tables, launch + optional hipEvent timing on the handle's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsl.h"
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+struct rsl_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<int, float2*> tw;  // N -> device table exp(-2 pi i k / N)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[RSL_K_COUNT];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  double ms[RSL_K_COUNT] = {0};
+  long long cnt[RSL_K_COUNT] = {0};
+};
+
+namespace {
+
+int fail(rsl_context* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  return code;
+}
+
+int hip_check(rsl_context* h, hipError_t e, const char* what) {
+  if (e == hipSuccess) return RSL_OK;
+  return fail(h, RSL_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct Scope {
+  rsl_context* h;
+  int kid;
+  hipEvent_t a = nullptr, b = nullptr;
+  Scope(rsl_context* h_, int kid_) : h(h_), kid(kid_) {
+    hipSetDevice(h->device);
+    if (h->timing) {
+      if (!h->ev_pool.empty()) {
+        a = h->ev_pool.back().first;
+        b = h->ev_pool.back().second;
+        h->ev_pool.pop_back();
+      } else {
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+      }
+      hipEventRecord(a, h->stream);
+    }
+  }
+  ~Scope() {
+    if (a) {
+      hipEventRecord(b, h->stream);
+      h->ev[kid].push_back({a, b});
+    }
+  }
+};
+
+float2* twiddles(rsl_context* h, int n) {
+  auto it = h->tw.find(n);
+  if (it != h->tw.end()) return it->second;
+  std::vector<float2> t(n);
+  for (int k = 0; k < n; ++k) {
+    const double ang = -2.0 * M_PI * (double)k / (double)n;
+    t[k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  }
+  float2* d = nullptr;
+  if (hipMalloc(&d, sizeof(float2) * n) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, t.data(), sizeof(float2) * n, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  h->tw[n] = d;
+  return d;
+}
+
+void collect(rsl_context* h) {
+  for (int k = 0; k < RSL_K_COUNT; ++k) {
+    for (auto& p : h->ev[k]) {
+      hipEventSynchronize(p.second);
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, p.first, p.second);
+      h->ms[k] += ms;
+      h->cnt[k] += 1;
+      h->ev_pool.push_back(p);
+    }
+    h->ev[k].clear();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsl_version(void) { return 1; }
+
+int rsl_fft_supported(int n) {
+  switch (n) {
+    case 8: case 16: case 32: case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096:
+    case 25: case 50: case 100: case 200: case 400: case 800: case 1600:
+      return 1;
+    default:
+      return 0;
+  }
+}
+
+int rsl_create(rsl_handle* out, int device) {
+  if (!out) return RSL_ERR_INVALID;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RSL_ERR_HIP;
+  rsl_context* h = new rsl_context();
+  h->device = device;
+  *out = h;
+  return RSL_OK;
+}
+
+int rsl_destroy(rsl_handle h) {
+  if (!h) return RSL_OK;
+  hipSetDevice(h->device);
+  for (auto& kv : h->tw) hipFree(kv.second);
+  for (int k = 0; k < RSL_K_COUNT; ++k)
+    for (auto& p : h->ev[k]) {
+      hipEventDestroy(p.first);
+      hipEventDestroy(p.second);
+    }
+  for (auto& p : h->ev_pool) {
+    hipEventDestroy(p.first);
+    hipEventDestroy(p.second);
+  }
+  delete h;
+  return RSL_OK;
+}
+
+const char* rsl_last_error(rsl_handle h) { return h ? h->err.c_str() : "null handle"; }
+
+int rsl_set_stream(rsl_handle h, void* s) {
+  if (!h) return RSL_ERR_INVALID;
+  h->stream = reinterpret_cast<hipStream_t>(s);
+  return RSL_OK;
+}
+
+int rsl_sync(rsl_handle h) {
+  if (!h) return RSL_ERR_INVALID;
+  hipSetDevice(h->device);
+  return hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+}
+
+int rsl_timing_enable(rsl_handle h, int on) {
+  if (!h) return RSL_ERR_INVALID;
+  h->timing = on != 0;
+  return RSL_OK;
+}
+
+int rsl_timing_reset(rsl_handle h) {
+  if (!h) return RSL_ERR_INVALID;
+  collect(h);
+  for (int k = 0; k < RSL_K_COUNT; ++k) {
+    h->ms[k] = 0;
+    h->cnt[k] = 0;
+  }
+  return RSL_OK;
+}
+
+int rsl_timing_read(rsl_handle h, int kid, double* total_ms, long long* launches) {
+  if (!h || kid < 0 || kid >= RSL_K_COUNT) return RSL_ERR_INVALID;
+  collect(h);
+  if (total_ms) *total_ms = h->ms[kid];
+  if (launches) *launches = h->cnt[kid];
+  return RSL_OK;
+}
+
+int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S, const void* table,
+            int dc_removal, void* work, void* rds) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || A <= 0 || S <= 0 || C <= 0 || chirp0 < 0 || chirp0 + C > C_total)
+    return fail(h, RSL_ERR_INVALID, "rsl_rds: bad shape");
+  if (!cube || !table || !work || !rds) return fail(h, RSL_ERR_INVALID, "rsl_rds: null pointer");
+  if (!rsl_fft_supported(S) || !rsl_fft_supported(C))
+    return fail(h, RSL_ERR_UNSUPPORTED, "rsl_rds: FFT size not supported (S=" + std::to_string(S) +
+                                            ", C=" + std::to_string(C) + ")");
+  if (F == 0) return RSL_OK;
+  hipSetDevice(h->device);
+  float2* tS = twiddles(h, S);
+  float2* tC = twiddles(h, C);
+  if (!tS || !tC) return fail(h, RSL_ERR_HIP, "twiddle table allocation failed");
+  bool sup = true;
+  hipError_t e;
+  {
+    Scope sc(h, RSL_K_RANGE_FFT);
+    e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
+                              dc_removal, (float2*)work, &sup);
+  }
+  if (int r = hip_check(h, e, "range_fft")) return r;
+  {
+    Scope sc(h, RSL_K_DOPPLER_FFT);
+    e = rsl::launch_doppler_fft(h->stream, (const float2*)work, F, A, C, S, tC, (float2*)rds, &sup);
+  }
+  return hip_check(h, e, "doppler_fft");
+}
+
+int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
+               void* mask, void* row_count, void* db_map) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || A <= 0 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_detect: bad shape");
+  if (!rds || !mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_detect: null pointer");
+  if ((size_t)(18 * (size_t)C * 4) > 64 * 1024) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_detect: C too large");
+  Scope sc(h, RSL_K_DETECT);
+  return hip_check(h,
+                   rsl::launch_detect(h->stream, (const float2*)rds, F, A, S, C, thr_power, i_lo, i_hi,
+                                      (unsigned long long*)mask, (int*)row_count, (float*)db_map),
+                   "detect");
+}
+
+int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int F, int A, int S, int C,
+                     void* entry_row_off, void* cell_row_off, void* scratch, void* entry_base, void* cell_base,
+                     void* frame_counts) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || A <= 0 || S <= 0 || C <= 0 || A > 32) return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: bad shape");
+  if (!mask || !row_count || !entry_row_off || !cell_row_off || !scratch || !entry_base || !cell_base || !frame_counts)
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: null pointer");
+  if (F == 0) {
+    hipSetDevice(h->device);
+    long long z = 0;
+    hipMemcpyAsync(entry_base, &z, 8, hipMemcpyHostToDevice, h->stream);
+    hipMemcpyAsync(cell_base, &z, 8, hipMemcpyHostToDevice, h->stream);
+    return hip_check(h, hipStreamSynchronize(h->stream), "offsets(F=0)");
+  }
+  Scope sc(h, RSL_K_OFFSETS);
+  return hip_check(h,
+                   rsl::launch_offsets(h->stream, (const unsigned long long*)mask, (const int*)row_count, F, A, S, C,
+                                       (int*)entry_row_off, (int*)cell_row_off, (int*)scratch,
+                                       (long long*)entry_base, (long long*)cell_base, (long long*)frame_counts),
+                   "offsets");
+}
+
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A, int S, int C,
+                  const void* entry_row_off, const void* cell_row_off, const void* entry_base, const void* cell_base,
+                  long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin, void* e_dbin, void* e_cell,
+                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: bad shape");
+  if (!rds || !mask || !entry_row_off || !cell_row_off || !entry_base || !cell_base)
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null pointer");
+  if ((entry_cap > 0 && (!e_ant || !e_rbin || !e_dbin || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null output");
+  Scope sc(h, RSL_K_EMIT);
+  return hip_check(h,
+                   rsl::launch_emit(h->stream, (const float2*)rds, (const unsigned long long*)mask, F, A, S, C,
+                                    (const int*)entry_row_off, (const int*)cell_row_off, (const long long*)entry_base,
+                                    (const long long*)cell_base, entry_cap, cell_cap, (int*)e_ant, (int*)e_rbin,
+                                    (int*)e_dbin, (int*)e_cell, (double*)e_pdb, (int*)c_frame, (int*)c_rc,
+                                    (unsigned*)c_amask),
+                   "emit");
+}
+
+long long rsl_steer_table_floats(int G, int M) {
+  if (G <= 0 || M <= 0) return 0;
+  const int KS = (2 * M + 3) / 4, KSG = (KS + 3) / 4;
+  const long long ntiles = (2LL * G + 15) / 16;
+  return ntiles * KSG * 64 * 4;
+}
+
+int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* ntiles_out) {
+  if (!steer || !out || G <= 0 || M <= 0 || M > 16) return RSL_ERR_INVALID;
+  const int KS = (2 * M + 3) / 4, KSG = (KS + 3) / 4;
+  const int ntiles = (2 * G + 15) / 16;
+  for (int t = 0; t < ntiles; ++t)
+    for (int sg = 0; sg < KSG; ++sg)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 4; ++e) {
+          const int s = 4 * sg + e;
+          const int i = lane & 15, qq = lane >> 4;
+          const int k = 4 * s + qq;
+          const int g = 8 * t + (i >> 1), part = i & 1;
+          double v = 0.0;
+          if (s < KS && g < G && k < 2 * M) {
+            const int m = k < M ? k : k - M;
+            const double ar = steer[((size_t)g * M + m) * 2], ai = steer[((size_t)g * M + m) * 2 + 1];
+            if (part == 0) v = k < M ? ar : ai;
+            else v = k < M ? -ai : ar;
+          }
+          out[(((size_t)t * KSG + sg) * 64 + lane) * 4 + e] = (float)v;
+        }
+  if (ntiles_out) *ntiles_out = ntiles;
+  return RSL_OK;
+}
+
+int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+            const void* ncell_dev, long long ncell, const void* steer_tab, int G, int method, void* out_idx,
+            void* out_gmax, void* out_spec) {
+  if (!h) return RSL_ERR_INVALID;
+  if (A <= 0 || A > 16 || S <= 0 || C <= 0 || G <= 0) return fail(h, RSL_ERR_INVALID, "rsl_doa: bad shape");
+  if (!rds || !c_frame || !c_rc || !steer_tab || !out_idx) return fail(h, RSL_ERR_INVALID, "rsl_doa: null pointer");
+  if (method != RSL_METHOD_MUSIC && method != RSL_METHOD_BEAMFORMING)
+    return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
+  if (!ncell_dev && ncell <= 0) return RSL_OK;
+  hipSetDevice(h->device);
+  int dev = h->device, ncu = 256;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  long long blocks = (long long)ncu * 4;
+  if (!ncell_dev) {
+    const long long need = (ncell + 127) / 128;  // 4 waves x 32 cells
+    if (need < blocks) blocks = need;
+  }
+  const int ntiles = (2 * G + 15) / 16;
+  Scope sc(h, RSL_K_DOA_SCAN);
+  return hip_check(h,
+                   rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
+                                        (const long long*)ncell_dev, ncell, (const float*)steer_tab, ntiles, G,
+                                        method == RSL_METHOD_MUSIC, (int*)out_idx, (float*)out_gmax,
+                                        (float*)out_spec, (int)blocks),
+                   "doa_scan");
+}
+
+int rsl_cell_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                    const void* ncell_dev, long long ncell, double esprit_scale, const void* gidx,
+                    const void* az_table, void* sig_out, void* esprit_deg, void* phase, void* az_out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_cell_extras: bad shape");
+  if (!rds || !c_frame || !c_rc) return fail(h, RSL_ERR_INVALID, "rsl_cell_extras: null pointer");
+  if (az_out && (!gidx || !az_table)) return fail(h, RSL_ERR_INVALID, "rsl_cell_extras: az_out needs gidx+table");
+  if (ncell <= 0) return RSL_OK;  // ncell is the launch bound (capacity) when ncell_dev is given
+  Scope sc(h, RSL_K_CELL_EXTRAS);
+  return hip_check(h,
+                   rsl::launch_cell_extras(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
+                                           (const int*)c_rc, (const long long*)ncell_dev, ncell, esprit_scale,
+                                           (const int*)gidx, (const double*)az_table, (float2*)sig_out,
+                                           (double*)esprit_deg, (double*)phase, (double*)az_out),
+                   "cell_extras");
+}
+
+int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                   long long n, const void* gidx, const void* steer_c128, const void* steer_phase, void* conf) {
+  if (!h) return RSL_ERR_INVALID;
+  if (A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_confidence: bad shape");
+  if (!rds || !c_frame || !c_rc || !gidx || !steer_c128 || !steer_phase || !conf)
+    return fail(h, RSL_ERR_INVALID, "rsl_confidence: null pointer");
+  Scope sc(h, RSL_K_CONFIDENCE);
+  return hip_check(h,
+                   rsl::launch_confidence(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
+                                          (const int*)c_rc, n, (const int*)gidx, (const double*)steer_c128,
+                                          (const double*)steer_phase, (double*)conf),
+                   "confidence");
+}
+
+int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask, const void* seg, int F, double k,
+                 double ridge, const double* bounds4, void* out, void* resid, void* pred) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || !az || !y || !seg || !bounds4 || !out) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
+  if (!(bounds4[0] <= bounds4[1]) || !(bounds4[2] <= bounds4[3]) || ridge < 0)
+    return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad bounds/ridge");
+  Scope sc(h, RSL_K_VELOCITY);
+  return hip_check(h,
+                   rsl::launch_velocity(h->stream, (const double*)az, (const double*)y, (const unsigned*)amask,
+                                        (const long long*)seg, F, k, ridge, bounds4, (double*)out, (double*)resid,
+                                        (double*)pred),
+                   "velocity");
+}
+
+}  // extern "C"

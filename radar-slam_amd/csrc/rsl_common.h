@@ -1,0 +1,214 @@
+// rsl_common.h — shared device helpers for the radar-slam MI355X kernels (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RSL_DEV __device__ __forceinline__
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+RSL_DEV float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+RSL_DEV float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+RSL_DEV float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+// multiply by -i : (x + iy)(-i) = y - ix
+RSL_DEV float2 cmul_mi(float2 a) { return make_float2(a.y, -a.x); }
+RSL_DEV float cabs2(float2 a) { return fmaf(a.x, a.x, a.y * a.y); }
+
+// ------------------------------------------------------------------------------------
+// Compile-time FFT plan: N = prod(radices), radices from {8,4,2,5,3,7}.
+// ------------------------------------------------------------------------------------
+struct FftPlan {
+  int n;
+  int r[16];
+  int ns[16];  // product of radices before stage s (Stockham "Ns")
+};
+
+constexpr FftPlan make_plan(int N) {
+  FftPlan p{0, {}, {}};
+  int m = N;
+  int ns = 1;
+  const int order[6] = {8, 4, 2, 5, 3, 7};
+  for (int oi = 0; oi < 6; ++oi) {
+    int R = order[oi];
+    while (m > 1 && m % R == 0) {
+      p.r[p.n] = R;
+      p.ns[p.n] = ns;
+      ns *= R;
+      m /= R;
+      p.n++;
+    }
+  }
+  if (m != 1) p.n = -1;  // unsupported prime factor
+  return p;
+}
+
+constexpr bool fft_supported(int N) { return N >= 2 && make_plan(N).n > 0; }
+
+// Forward DFT of R points held in registers (natural order in/out), sign exp(-2 pi i nk/R).
+template <int R>
+struct Dft;
+
+template <>
+struct Dft<2> {
+  RSL_DEV static void run(float2* v) {
+    float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+
+template <>
+struct Dft<4> {
+  RSL_DEV static void run(float2* v) {
+    float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    float2 t2 = cadd(v[1], v[3]), t3 = cmul_mi(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  }
+};
+
+template <>
+struct Dft<8> {
+  RSL_DEV static void run(float2* v) {
+    const float h = 0.70710678118654752440f;
+    // DIF radix-2 split: even outputs from a_n + a_{n+4}, odd from (a_n - a_{n+4}) W8^n
+    float2 e[4], o[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      e[n] = cadd(v[n], v[n + 4]);
+      o[n] = csub(v[n], v[n + 4]);
+    }
+    // W8^1 = (h, -h), W8^2 = -i, W8^3 = (-h, -h)
+    o[1] = make_float2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+    o[2] = cmul_mi(o[2]);
+    o[3] = make_float2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+    Dft<4>::run(e);
+    Dft<4>::run(o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = e[k];
+      v[2 * k + 1] = o[k];
+    }
+  }
+};
+
+// Generic small-prime DFT (R = 3, 5, 7) with exact literal roots of unity.
+template <int R>
+struct Roots;
+template <>
+struct Roots<3> {
+  RSL_DEV static float c(int m) {
+    const float t[3] = {1.f, -0.5f, -0.5f};
+    return t[m];
+  }
+  RSL_DEV static float s(int m) {
+    const float t[3] = {0.f, -0.86602540378443864676f, 0.86602540378443864676f};
+    return t[m];
+  }
+};
+template <>
+struct Roots<5> {
+  RSL_DEV static float c(int m) {
+    const float t[5] = {1.f, 0.30901699437494742410f, -0.80901699437494742410f, -0.80901699437494742410f,
+                        0.30901699437494742410f};
+    return t[m];
+  }
+  RSL_DEV static float s(int m) {
+    const float t[5] = {0.f, -0.95105651629515357212f, -0.58778525229247312917f, 0.58778525229247312917f,
+                        0.95105651629515357212f};
+    return t[m];
+  }
+};
+template <>
+struct Roots<7> {
+  RSL_DEV static float c(int m) {
+    const float t[7] = {1.f, 0.62348980185873353053f, -0.22252093395631440429f, -0.90096886790241912624f,
+                        -0.90096886790241912624f, -0.22252093395631440429f, 0.62348980185873353053f};
+    return t[m];
+  }
+  RSL_DEV static float s(int m) {
+    const float t[7] = {0.f, -0.78183148246802980871f, -0.97492791218182360702f, -0.43388373911755812048f,
+                        0.43388373911755812048f, 0.97492791218182360702f, 0.78183148246802980871f};
+    return t[m];
+  }
+};
+
+template <int R>
+struct Dft {
+  RSL_DEV static void run(float2* v) {
+    float2 out[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      float2 acc = v[0];
+#pragma unroll
+      for (int n = 1; n < R; ++n) {
+        const int m = (n * k) % R;
+        const float2 w = make_float2(Roots<R>::c(m), Roots<R>::s(m));
+        acc = cadd(acc, cmul(v[n], w));
+      }
+      out[k] = acc;
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) v[k] = out[k];
+  }
+};
+
+// One Stockham autosort stage over ROWS independent rows of N points held in LDS
+// (row stride LD complex).  tw[k] = exp(-2 pi i k / N), k < N (fp64-accurate table).
+// In place: every thread reads its butterflies' inputs, the block syncs, then writes.
+template <int N, int R, int NS, int ROWS, int NT, int LD>
+RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
+  constexpr int NB = N / R;
+  constexpr int TOT = ROWS * NB;
+  constexpr int PER = (TOT + NT - 1) / NT;
+  float2 v[PER][R];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    if ((TOT % NT) == 0 || idx < TOT) {
+      const int row = idx / NB, j = idx - (idx / NB) * NB;
+      const float2* src = buf + row * LD;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[q][r] = src[j + r * NB];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    if ((TOT % NT) == 0 || idx < TOT) {
+      const int row = idx / NB, j = idx - (idx / NB) * NB;
+      const int k = j % NS;
+      if (NS > 1) {
+        constexpr int STEP = N / (NS * R);
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[r * k * STEP]);
+      }
+      Dft<R>::run(v[q]);
+      float2* dst = buf + row * LD + (j / NS) * NS * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[r * NS] = v[q][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int N, int S, int ROWS, int NT, int LD>
+RSL_DEV void fft_run(float2* buf, const float2* tw, int tid) {
+  constexpr FftPlan P = make_plan(N);
+  if constexpr (S < P.n) {
+    fft_stage<N, P.r[S], P.ns[S], ROWS, NT, LD>(buf, tw, tid);
+    fft_run<N, S + 1, ROWS, NT, LD>(buf, tw, tid);
+  }
+}
+
+// Forward N-point FFT of ROWS rows in LDS.  Caller must __syncthreads() before.
+template <int N, int ROWS, int NT, int LD>
+RSL_DEV void fft_rows(float2* buf, const float2* tw, int tid) {
+  static_assert(make_plan(N).n > 0, "unsupported FFT size");
+  fft_run<N, 0, ROWS, NT, LD>(buf, tw, tid);
+}

@@ -1,0 +1,261 @@
+// rsl_detect.hip — K3 peak detection and order-preserving compaction for gfx950.
+//
+// Replaces SignalPreprocessor.extract_range_doppler_peaks (reference src/radar_signal/dechirp.py:215-278):
+//   db = 10 log10(|rds|^2 + 1e-12); peak = (maximum_filter(db, 3, mode='reflect') == db) & (db > thr)
+//   & (min_range <= range_m[i] <= max_range); peaks listed antenna -> range -> doppler (np.where order).
+// The 3x3 test runs on fp32 power p (log10 is monotone); 'reflect' boundary duplicates the edge cell,
+// so out-of-range neighbours simply do not take part.  The threshold is evaluated as
+// (double)p > 10^(thr/10) - 1e-12 and the range gate as an index interval, both precomputed in fp64.
+// Per-antenna 64-bit ballots give one mask word per 64 Doppler cells; a per-frame scan then turns
+// row counts into entry offsets (antenna-major) and union-cell offsets (range-major), and the emit
+// kernel writes both lists in reference order without any sort.
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+namespace rsl {
+
+constexpr int kDetRows = 16;  // shifted range rows per workgroup
+
+__global__ __launch_bounds__(256) void k_detect(const float2* __restrict__ rds, int S, int C, int W, double thr_p,
+                                                int i_lo, int i_hi, unsigned long long* __restrict__ mask,
+                                                int* __restrict__ row_count, float* __restrict__ dbmap) {
+  extern __shared__ float pw[];  // (kDetRows + 2) x C power values
+  const int nib = (S + kDetRows - 1) / kDetRows;
+  const int ib = blockIdx.x % nib;
+  const long fa = blockIdx.x / nib;
+  const int i0 = ib * kDetRows;
+  const int nrows = min(kDetRows, S - i0);
+  const float2* base = rds + (size_t)fa * S * C;
+  for (int idx = threadIdx.x; idx < (nrows + 2) * C; idx += 256) {
+    const int r = idx / C, j = idx - r * C;
+    const int i = i0 - 1 + r;
+    pw[idx] = (i >= 0 && i < S) ? cabs2(base[(size_t)i * C + j]) : -1.f;  // -1: outside (no neighbour)
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = wave; r < nrows; r += 4) {
+    const int i = i0 + r;
+    const bool gate = (i >= i_lo && i <= i_hi);
+    const float* up = pw + r * C;
+    const float* mid = up + C;
+    const float* dn = mid + C;
+    int cnt = 0;
+    for (int w = 0; w < W; ++w) {
+      const int j = w * 64 + lane;
+      bool pk = false;
+      if (j < C) {
+        const float p = mid[j];
+        pk = gate && ((double)p > thr_p);
+        const bool hasl = j > 0, hasr = j + 1 < C;
+        float m = fmaxf(up[j], dn[j]);
+        if (hasl) m = fmaxf(m, fmaxf(mid[j - 1], fmaxf(up[j - 1], dn[j - 1])));
+        if (hasr) m = fmaxf(m, fmaxf(mid[j + 1], fmaxf(up[j + 1], dn[j + 1])));
+        pk = pk && (p >= m);
+        if (dbmap) dbmap[((size_t)fa * S + i) * C + j] = 10.f * log10f(p + 1e-12f);
+      }
+      const unsigned long long b = __ballot(pk);
+      if (lane == 0) mask[((size_t)fa * S + i) * W + w] = b;
+      cnt += __popcll(b);
+    }
+    if (lane == 0) row_count[(size_t)fa * S + i] = cnt;
+  }
+}
+
+// Exclusive scan of n ints (global) into out (global) by one 1024-thread block; returns total.
+__device__ long long block_scan_global(const int* in, int* out, int n, long long* lds) {
+  const int t = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int b = t * per, e = min(n, b + per);
+  long long s = 0;
+  for (int k = b; k < e; ++k) s += in[k];
+  lds[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const long long v = (t >= off) ? lds[t - off] : 0;
+    __syncthreads();
+    lds[t] += v;
+    __syncthreads();
+  }
+  long long run = lds[t] - s;
+  const long long total = lds[1023];
+  for (int k = b; k < e; ++k) {
+    const int v = in[k];
+    out[k] = (int)run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+// One block per frame: entry offsets over (antenna, range) rows and union-cell offsets over range rows.
+__global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __restrict__ mask,
+                                                  const int* __restrict__ row_count, int A, int S, int W,
+                                                  int* __restrict__ entry_row_off, int* __restrict__ cell_row_off,
+                                                  int* __restrict__ cell_row_cnt, long long* __restrict__ frame_counts) {
+  __shared__ long long lds[1024];
+  const long f = blockIdx.x;
+  const long long te = block_scan_global(row_count + f * A * S, entry_row_off + f * A * S, A * S, lds);
+  const unsigned long long* mf = mask + (size_t)f * A * S * W;
+  for (int i = threadIdx.x; i < S; i += 1024) {
+    int c = 0;
+    for (int w = 0; w < W; ++w) {
+      unsigned long long u = 0;
+      for (int a = 0; a < A; ++a) u |= mf[((size_t)a * S + i) * W + w];
+      c += __popcll(u);
+    }
+    cell_row_cnt[f * S + i] = c;
+  }
+  __syncthreads();
+  const long long tc = block_scan_global(cell_row_cnt + f * S, cell_row_off + f * S, S, lds);
+  if (threadIdx.x == 0) {
+    frame_counts[2 * f] = te;
+    frame_counts[2 * f + 1] = tc;
+  }
+}
+
+// One block: exclusive scan over frames -> entry_base[F+1], cell_base[F+1].
+__global__ __launch_bounds__(1024) void k_frame_scan(const long long* __restrict__ frame_counts, int F,
+                                                     long long* __restrict__ entry_base,
+                                                     long long* __restrict__ cell_base) {
+  __shared__ long long le[1024], lc[1024];
+  const int t = threadIdx.x;
+  const int per = (F + 1023) / 1024;
+  const int b = t * per, e = min(F, b + per);
+  long long se = 0, sc = 0;
+  for (int k = b; k < e; ++k) {
+    se += frame_counts[2 * k];
+    sc += frame_counts[2 * k + 1];
+  }
+  le[t] = se;
+  lc[t] = sc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const long long ve = (t >= off) ? le[t - off] : 0, vc = (t >= off) ? lc[t - off] : 0;
+    __syncthreads();
+    le[t] += ve;
+    lc[t] += vc;
+    __syncthreads();
+  }
+  long long re = le[t] - se, rc = lc[t] - sc;
+  for (int k = b; k < e; ++k) {
+    entry_base[k] = re;
+    cell_base[k] = rc;
+    re += frame_counts[2 * k];
+    rc += frame_counts[2 * k + 1];
+  }
+  if (t == 1023) {
+    entry_base[F] = le[1023];
+    cell_base[F] = lc[1023];
+  }
+}
+
+// One thread per (frame, range row, mask word).
+__global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, const unsigned long long* __restrict__ mask,
+                                              int F, int A, int S, int C, int W,
+                                              const int* __restrict__ entry_row_off, const int* __restrict__ cell_row_off,
+                                              const long long* __restrict__ entry_base,
+                                              const long long* __restrict__ cell_base, long long entry_cap,
+                                              long long cell_cap, int* __restrict__ e_ant, int* __restrict__ e_rbin,
+                                              int* __restrict__ e_dbin, int* __restrict__ e_cell,
+                                              double* __restrict__ e_pdb, int* __restrict__ c_frame,
+                                              int* __restrict__ c_rc, unsigned* __restrict__ c_amask) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long)F * S * W) return;
+  const int w = gid % W;
+  const int i = (gid / W) % S;
+  const long f = gid / ((long)W * S);
+  const unsigned long long* mf = mask + (size_t)f * A * S * W;
+  unsigned long long u = 0;
+  int cpre = 0;
+  for (int ww = 0; ww <= w; ++ww) {
+    unsigned long long uu = 0;
+    for (int a = 0; a < A; ++a) uu |= mf[((size_t)a * S + i) * W + ww];
+    if (ww < w) cpre += __popcll(uu);
+    else u = uu;
+  }
+  if (u == 0) return;
+  const long long cb = cell_base[f] + cell_row_off[f * S + i] + cpre;
+  // cells
+  {
+    unsigned long long m = u;
+    long long c = cb;
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      if (c < cell_cap) {
+        const int j = w * 64 + bit;
+        unsigned am = 0;
+        for (int a = 0; a < A; ++a) am |= (unsigned)((mf[((size_t)a * S + i) * W + w] >> bit) & 1ull) << a;
+        c_frame[c] = (int)f;
+        c_rc[c] = i * C + j;
+        c_amask[c] = am;
+      }
+      ++c;
+    }
+  }
+  // entries, antenna by antenna
+  const float2* rf = rds + (size_t)f * A * S * C;
+  for (int a = 0; a < A; ++a) {
+    const unsigned long long* row = mf + ((size_t)a * S + i) * W;
+    unsigned long long m = row[w];
+    if (!m) continue;
+    int epre = 0;
+    for (int ww = 0; ww < w; ++ww) epre += __popcll(row[ww]);
+    long long e = entry_base[f] + entry_row_off[f * A * S + (long)a * S + i] + epre;
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      if (e < entry_cap) {
+        const int j = w * 64 + bit;
+        e_ant[e] = a;
+        e_rbin[e] = i;
+        e_dbin[e] = j;
+        e_cell[e] = (int)(cb + __popcll(u & ((1ull << bit) - 1ull)));
+        if (e_pdb) {
+          const float p = cabs2(rf[((size_t)a * S + i) * C + j]);
+          e_pdb[e] = 10.0 * log10((double)p + 1e-12);
+        }
+      }
+      ++e;
+    }
+  }
+}
+
+hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
+                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap) {
+  if (F <= 0 || A <= 0 || S <= 0 || C <= 0) return hipSuccess;
+  const int W = (C + 63) / 64;
+  const long nblk = (long)F * A * ((S + kDetRows - 1) / kDetRows);
+  const size_t lds = sizeof(float) * (kDetRows + 2) * (size_t)C;
+  hipLaunchKernelGGL(k_detect, dim3((unsigned)nblk), dim3(256), lds, st, rds, S, C, W, thr_p, i_lo, i_hi, mask,
+                     row_count, dbmap);
+  return hipGetLastError();
+}
+
+hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const int* row_count, int F, int A, int S,
+                          int C, int* entry_row_off, int* cell_row_off, int* cell_row_cnt, long long* entry_base,
+                          long long* cell_base, long long* frame_counts) {
+  if (F <= 0) return hipSuccess;
+  const int W = (C + 63) / 64;
+  hipLaunchKernelGGL(k_offsets, dim3(F), dim3(1024), 0, st, mask, row_count, A, S, W, entry_row_off, cell_row_off,
+                     cell_row_cnt, frame_counts);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_frame_scan, dim3(1), dim3(1024), 0, st, frame_counts, F, entry_base, cell_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long long* mask, int F, int A, int S, int C,
+                       const int* entry_row_off, const int* cell_row_off, const long long* entry_base,
+                       const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
+                       int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
+  if (F <= 0) return hipSuccess;
+  const int W = (C + 63) / 64;
+  const long n = (long)F * S * W;
+  hipLaunchKernelGGL(k_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rds, mask, F, A, S, C, W,
+                     entry_row_off, cell_row_off, entry_base, cell_base, entry_cap, cell_cap, e_ant, e_rbin, e_dbin,
+                     e_cell, e_pdb, c_frame, c_rc, c_amask);
+  return hipGetLastError();
+}
+
+}  // namespace rsl

@@ -1,0 +1,344 @@
+// rsl_doa.hip — K4..K7: signature gather, MFMA steering scan (MUSIC / beamforming argmax), ESPRIT,
+// spatial phase, robust confidence.  gfx950 / CDNA4.
+//
+// Replaces (reference src/angle_estimation/angle_estimation.py):
+//   extract_spatial_signature :67-90, music_spectrum :109-154, estimate_angle_music :156-176,
+//   estimate_angle_esprit :178-225, estimate_angle_beamforming :227-251,
+// and robust_angle_estimation.py compute_angle_confidence :88-138, estimate_angle_robust :220-272.
+//
+// MUSIC in the reference is rank-1 (R = s s^H from one normalised snapshot), so with E_n the M-1
+// noise eigenvectors, |a^H E_n E_n^H a| = M - |a^H s|^2 exactly; MUSIC and beamforming share the one
+// dense contraction G = |A^H S|^2 (A: [G x M] steering table, S: [M x cells]).  It is run as a real
+// GEMM on v_mfma_f32_16x16x4_f32 (exact fp32, bitwise an fmaf chain): steering rows are stacked
+// [Re; Im] per grid point ([ar, ai] and [-ai, ar] against the column [sr; si]), so lane (q, col)
+// of a 16x16 accumulator holds Re/Im of two grid points of one cell and folds |.|^2 + argmax
+// in registers.  The steering operand lives in LDS in per-lane MFMA order (one ds_read_b128 per
+// tile); 32 cells per wave per pass give two independent accumulator chains.
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+namespace rsl {
+
+template <int KS>
+__global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds, int A, int S, int C,
+                                                  const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                  const long long* __restrict__ ncell_dev, long long ncell_host,
+                                                  const float4* __restrict__ steer, int ntiles, int G, int music,
+                                                  int use_lds, int* __restrict__ out_idx,
+                                                  float* __restrict__ out_gmax, float* __restrict__ out_spec) {
+  constexpr int KSG = (KS + 3) / 4;
+  extern __shared__ float4 sst[];
+  const float4* st = steer;
+  if (use_lds) {
+    for (int x = threadIdx.x; x < ntiles * KSG * 64; x += 256) sst[x] = steer[x];
+    __syncthreads();
+    st = sst;
+  }
+  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, jj = lane & 15;
+  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
+  const float Mf = (float)A;
+  const long long nch = (ncell + 31) >> 5;
+  for (long long ch = (long long)blockIdx.x * 4 + wave; ch < nch; ch += (long long)gridDim.x * 4) {
+    float b[2][KS];
+    float pz[2];
+    bool ok[2];
+    long long cidx[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const long long c = ch * 32 + t2 * 16 + jj;
+      cidx[t2] = c;
+      ok[t2] = c < ncell;
+      const float2* base = rds;
+      if (ok[t2]) base = rds + (size_t)cfr[c] * fstride + crc[c];
+      float acc = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k = 4 * s + q;
+        float v = 0.f;
+        if (ok[t2] && k < 2 * A) {
+          const int m = k < A ? k : k - A;
+          const float2 z = base[(size_t)m * plane];
+          v = k < A ? z.x : z.y;
+        }
+        b[t2][s] = v;
+        acc = fmaf(v, v, acc);
+      }
+      acc += __shfl_xor(acc, 16);
+      acc += __shfl_xor(acc, 32);
+      pz[t2] = acc;
+      const float sc = acc > 0.f ? 1.0f / sqrtf(acc) : 1.0f;  // angle_estimation.py:86-88
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[t2][s] *= sc;
+    }
+    float best[2] = {-INFINITY, -INFINITY};
+    float bestg[2] = {0.f, 0.f};
+    int bidx[2] = {0, 0};
+    for (int t = 0; t < ntiles; ++t) {
+      float a[KSG * 4];
+#pragma unroll
+      for (int sg = 0; sg < KSG; ++sg) {
+        const float4 v = st[(t * KSG + sg) * 64 + lane];
+        a[4 * sg + 0] = v.x;
+        a[4 * sg + 1] = v.y;
+        a[4 * sg + 2] = v.z;
+        a[4 * sg + 3] = v.w;
+      }
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[0][s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[1][s], acc1, 0, 0, 0);
+      }
+      const int g0 = 8 * t + 2 * q;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const floatx4 acc = t2 ? acc1 : acc0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int g = g0 + h;
+          const float re = acc[2 * h], im = acc[2 * h + 1];
+          const float gv = fmaf(re, re, im * im);
+          const float den = Mf - gv;
+          const float key = music ? ((den > 1e-12f) ? gv : -1.f) : gv;
+          if (g < G && key > best[t2]) {
+            best[t2] = key;
+            bestg[t2] = gv;
+            bidx[t2] = g;
+          }
+          if (out_spec && ok[t2] && g < G) {
+            float val = gv;
+            if (music) {
+              const float d = (pz[t2] > 0.f) ? den : (Mf - 1.f);
+              val = (d > 1e-12f) ? 1.0f / d : 0.f;  // angle_estimation.py:149-152
+            }
+            out_spec[(size_t)cidx[t2] * G + g] = val;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+      for (int off = 16; off <= 32; off <<= 1) {
+        const float ob = __shfl_xor(best[t2], off);
+        const float og = __shfl_xor(bestg[t2], off);
+        const int oi = __shfl_xor(bidx[t2], off);
+        if (ob > best[t2] || (ob == best[t2] && oi < bidx[t2])) {  // first index wins (np.argmax)
+          best[t2] = ob;
+          bestg[t2] = og;
+          bidx[t2] = oi;
+        }
+      }
+      if (q == 0 && ok[t2]) {
+        out_idx[cidx[t2]] = bidx[t2];
+        if (out_gmax) out_gmax[cidx[t2]] = bestg[t2];
+      }
+    }
+  }
+}
+
+hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                           const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,
+                           int ntiles, int G, int music, int* out_idx, float* out_gmax, float* out_spec,
+                           int grid_blocks) {
+  const int KS = (2 * A + 3) / 4;
+  const int KSG = (KS + 3) / 4;
+  const size_t tab_bytes = (size_t)ntiles * KSG * 64 * sizeof(float4);
+  const int use_lds = tab_bytes <= 60 * 1024;
+  const size_t lds = use_lds ? tab_bytes : 0;
+  const float4* stp = reinterpret_cast<const float4*>(steer_tab);
+  switch (KS) {
+#define CASE(n)                                                                                                   \
+  case n:                                                                                                         \
+    hipLaunchKernelGGL(k_doa_scan<n>, dim3(grid_blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc,      \
+                       ncell_dev, ncell_host, stp, ntiles, G, music, use_lds, out_idx, out_gmax, out_spec);      \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-cell extras in fp64 from the fp32 RDS: normalised signature (angle_estimation.py:83-88),
+// ESPRIT closed form (angle_estimation.py:178-225), spatial phase angle(s1 conj(s0))
+// (velocity_solver.py:136), azimuth lookup from the argmax grid index.
+//
+// ESPRIT: svd of X = [s[:-1], s[1:]] -> U[:,0] = u ∝ X v with v the principal eigenvector of the
+// 2x2 Hermitian X^H X; pinv(U1) U2 = u[:-1]^H u[1:] / u[:-1]^H u[:-1]; the scale/phase of u cancels.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxA = 32;
+
+__global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ rds, int A, int S, int C,
+                                                     const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                     const long long* __restrict__ ncell_dev, long long ncell_host,
+                                                     double esprit_scale, const int* __restrict__ gidx,
+                                                     const double* __restrict__ az_table, float2* __restrict__ sig_out,
+                                                     double* __restrict__ esprit_deg, double* __restrict__ phase,
+                                                     double* __restrict__ az_out) {
+  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= ncell) return;
+  const size_t plane = (size_t)S * C;
+  const float2* base = rds + (size_t)cfr[c] * A * plane + crc[c];
+  double sr[kMaxA], si[kMaxA];
+  double pw = 0.0;
+  for (int m = 0; m < A; ++m) {
+    const float2 z = base[(size_t)m * plane];
+    sr[m] = z.x;
+    si[m] = z.y;
+    pw += sr[m] * sr[m] + si[m] * si[m];
+  }
+  if (pw > 0.0) {
+    const double sc = 1.0 / sqrt(pw);
+    for (int m = 0; m < A; ++m) {
+      sr[m] *= sc;
+      si[m] *= sc;
+    }
+  }
+  if (sig_out)
+    for (int m = 0; m < A; ++m) sig_out[(size_t)c * A + m] = make_float2((float)sr[m], (float)si[m]);
+  if (phase) {
+    // s1 * conj(s0)
+    const double re = sr[1] * sr[0] + si[1] * si[0];
+    const double im = si[1] * sr[0] - sr[1] * si[0];
+    phase[c] = atan2(im, re);
+  }
+  if (az_out && gidx) az_out[c] = az_table[gidx[c]];
+  if (esprit_deg) {
+    double a = 0, cc = 0, br = 0, bi = 0;
+    for (int m = 0; m + 1 < A; ++m) {
+      a += sr[m] * sr[m] + si[m] * si[m];
+      cc += sr[m + 1] * sr[m + 1] + si[m + 1] * si[m + 1];
+      // conj(x0) * x1
+      br += sr[m] * sr[m + 1] + si[m] * si[m + 1];
+      bi += sr[m] * si[m + 1] - si[m] * sr[m + 1];
+    }
+    const double hd = 0.5 * (a - cc);
+    const double l1 = 0.5 * (a + cc) + sqrt(hd * hd + br * br + bi * bi);
+    double v0r, v0i, v1r, v1i;
+    if (a >= cc) {  // v = [l1 - c, conj(b)]
+      v0r = l1 - cc; v0i = 0.0; v1r = br; v1i = -bi;
+    } else {        // v = [b, l1 - a]
+      v0r = br; v0i = bi; v1r = l1 - a; v1i = 0.0;
+    }
+    // u_m = v0 * s_m + v1 * s_{m+1}, m < A-1 ; phi = sum conj(u_m) u_{m+1} / sum |u_m|^2, m < A-2
+    double nr = 0, ni = 0, dd = 0;
+    double upr = 0, upi = 0;
+    for (int m = 0; m + 1 < A; ++m) {
+      const double ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
+      const double ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
+      if (m > 0) {
+        nr += upr * ur + upi * ui;
+        ni += upr * ui - upi * ur;
+        dd += upr * upr + upi * upi;
+      }
+      upr = ur;
+      upi = ui;
+    }
+    double ang = 0.0;
+    if (dd > 0.0) ang = atan2(ni / dd, nr / dd);
+    esprit_deg[c] = asin(ang * esprit_scale) * (180.0 / 3.14159265358979323846);
+  }
+}
+
+hipError_t launch_cell_extras(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                              const int* c_rc, const long long* ncell_dev, long long ncell_host, double esprit_scale,
+                              const int* gidx, const double* az_table, float2* sig_out, double* esprit_deg,
+                              double* phase, double* az_out) {
+  if (A > kMaxA) return hipErrorInvalidValue;
+  if (ncell_host <= 0) return hipSuccess;
+  const long long nb = (ncell_host + 255) / 256;
+  hipLaunchKernelGGL(k_cell_extras, dim3((unsigned)nb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
+                     ncell_host, esprit_scale, gidx, az_table, sig_out, esprit_deg, phase, az_out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Robust confidence (robust_angle_estimation.py:88-138), one thread per (cell, grid index):
+//   0.4 |a^H s|/||s|| + 0.3 exp(-mean |wrap(arg s - arg a)|) + 0.3 min(1, log10(mean p / pct20(p)) / 3)
+// clipped to [0, 1]; percentile is numpy 'linear' (index 0.2 (M-1)).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_confidence(const float2* __restrict__ rds, int A, int S, int C,
+                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                    long long n, const int* __restrict__ gidx,
+                                                    const double* __restrict__ steer,  // complex [G][A]
+                                                    const double* __restrict__ sphase,  // [G][A] np.angle(a)
+                                                    double* __restrict__ conf_out) {
+  const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= n) return;
+  const size_t plane = (size_t)S * C;
+  const float2* base = rds + (size_t)cfr[c] * A * plane + crc[c];
+  double sr[kMaxA], si[kMaxA], p[kMaxA];
+  double pw = 0.0;
+  for (int m = 0; m < A; ++m) {
+    const float2 z = base[(size_t)m * plane];
+    sr[m] = z.x;
+    si[m] = z.y;
+    pw += sr[m] * sr[m] + si[m] * si[m];
+  }
+  if (pw > 0.0) {  // process_targets_robust normalises first (robust_angle_estimation.py:374-377)
+    const double sc = 1.0 / sqrt(pw);
+    for (int m = 0; m < A; ++m) {
+      sr[m] *= sc;
+      si[m] *= sc;
+    }
+  }
+  const int g = gidx[c];
+  const double* a = steer + (size_t)g * A * 2;
+  const double* ap = sphase + (size_t)g * A;
+  double cr = 0, ci = 0, sp = 0, perr = 0, pm = 0;
+  for (int m = 0; m < A; ++m) {
+    const double ar = a[2 * m], ai = a[2 * m + 1];
+    cr += ar * sr[m] + ai * si[m];
+    ci += ar * si[m] - ai * sr[m];
+    p[m] = sr[m] * sr[m] + si[m] * si[m];
+    sp += p[m];
+    pm += p[m];
+    double d = atan2(si[m], sr[m]) - ap[m];
+    d = atan2(sin(d), cos(d));  // np.angle(np.exp(1j*d))
+    perr += fabs(d);
+  }
+  const double corr = sqrt(cr * cr + ci * ci);
+  const double ncorr = sp > 0 ? corr / sqrt(sp) : 0.0;
+  const double pc = exp(-perr / A);
+  // percentile 20, linear: sort p ascending (insertion sort, A <= 32)
+  for (int i = 1; i < A; ++i) {
+    const double v = p[i];
+    int j = i - 1;
+    while (j >= 0 && p[j] > v) {
+      p[j + 1] = p[j];
+      --j;
+    }
+    p[j + 1] = v;
+  }
+  const double vi = 0.2 * (A - 1);
+  const int lo = (int)floor(vi);
+  const int hi = lo + 1 < A ? lo + 1 : A - 1;
+  const double tfr = vi - lo;
+  double nf = (tfr >= 0.5) ? p[hi] - (p[hi] - p[lo]) * (1.0 - tfr) : p[lo] + (p[hi] - p[lo]) * tfr;
+  double snrc = 0.0;
+  if (nf > 0) {
+    snrc = log10((pm / A) / nf) / 3.0;
+    if (snrc > 1.0) snrc = 1.0;
+  }
+  double conf = ncorr * 0.4 + pc * 0.3 + snrc * 0.3;
+  conf = fmin(1.0, fmax(0.0, conf));
+  conf_out[c] = conf;
+}
+
+hipError_t launch_confidence(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                             const int* c_rc, long long n, const int* gidx, const double* steer_c128,
+                             const double* steer_phase, double* conf_out) {
+  if (A > kMaxA) return hipErrorInvalidValue;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_confidence, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
+                     n, gidx, steer_c128, steer_phase, conf_out);
+  return hipGetLastError();
+}
+
+}  // namespace rsl

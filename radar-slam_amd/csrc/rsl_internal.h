@@ -1,0 +1,49 @@
+// rsl_internal.h — launcher declarations shared between the kernel files and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsl {
+
+// K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
+// cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
+hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
+                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported);
+// K2: Doppler FFT (C points) + fftshift on both axes, transposed store.
+// work c64 [F, A, C, S] -> rds c64 [F, A, S, C]
+hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
+                              float2* rds, bool* supported);
+
+// K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
+hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
+                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap);
+// Per-frame offsets of peak entries (antenna-major) and union cells (range-major).
+hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const int* row_count, int F, int A, int S,
+                          int C, int* entry_row_off, int* cell_row_off, int* cell_row_cnt, long long* entry_base,
+                          long long* cell_base, long long* frame_counts);
+// Emit compacted entries and cells in reference order.
+hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long long* mask, int F, int A, int S, int C,
+                       const int* entry_row_off, const int* cell_row_off, const long long* entry_base,
+                       const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
+                       int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
+
+// K5: steering scan on MFMA (f32 16x16x4), argmax; optional spectrum.
+hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                           const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,
+                           int ntiles, int G, int music, int* out_idx, float* out_gmax, float* out_spec,
+                           int grid_blocks);
+// K4/K6: normalised signature, ESPRIT closed form (fp64), spatial phase, azimuth lookup.
+hipError_t launch_cell_extras(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                              const int* c_rc, const long long* ncell_dev, long long ncell_host, double esprit_scale,
+                              const int* gidx, const double* az_table, float2* sig_out, double* esprit_deg,
+                              double* phase, double* az_out);
+// K7: robust confidence for (cell, grid index) pairs (fp64).
+hipError_t launch_confidence(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                             const int* c_rc, long long n, const int* gidx, const double* steer_c128,
+                             const double* steer_phase, double* conf_out);
+// K8: batched bounded / ridge least squares velocity solve, one segment per frame.
+hipError_t launch_velocity(hipStream_t st, const double* az, const double* y, const unsigned* amask,
+                           const long long* seg, int F, double k, double ridge, const double* bounds4, double* out,
+                           double* resid, double* pred);
+
+}  // namespace rsl

@@ -1,0 +1,157 @@
+// rsl_vel.hip — K8: batched box-constrained (ridge) least-squares velocity solve, fp64.  gfx950.
+//
+// Replaces VelocitySolver.two_step_optimization (reference src/velocity_solver/velocity_solver.py:178-307),
+// which runs differential_evolution (seed 42) over cost = sum (y - 4 pi dt / lambda * (v + w x p).d)^2
+// (velocity_solver.py:65-176).  With elevation 0 and p = r d (velocity_solver.py:334-339), (w x p).d = 0 and
+// d_z = 0: only (v_x, v_y) enter, linearly.  The cost is a convex quadratic over the box
+// [-50,50]^2, so its exact minimiser is the interior normal-equation solution when feasible, else the
+// best of the four edge minimisers (1-D clamp).  ``ridge`` adds ridge*(vx^2+vy^2)
+// (velocity_solver_improved.py:261 without the wrap).  Items carry a multiplicity (popcount of the
+// antenna mask of a deduplicated cell) so duplicate per-antenna detections count as in the reference.
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+namespace rsl {
+
+__device__ double block_sum(double v, double* sh) {
+  const int t = threadIdx.x;
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+  __syncthreads();
+  if ((t & 63) == 0) sh[t >> 6] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (t == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r += sh[w];
+  __syncthreads();
+  return r;  // valid on thread 0
+}
+
+__device__ double block_max(double v, double* sh) {
+  const int t = threadIdx.x;
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off));
+  __syncthreads();
+  if ((t & 63) == 0) sh[t >> 6] = v;
+  __syncthreads();
+  double r = -1.0;
+  if (t == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = fmax(r, sh[w]);
+  __syncthreads();
+  return r;
+}
+
+__device__ double qcost(double vx, double vy, double k, double ridge, const double* m) {
+  // m: [n, cc, cs, ss, cy, sy, yy]
+  const double kx = k * vx, ky = k * vy;
+  return m[6] - 2.0 * (kx * m[4] + ky * m[5]) + kx * kx * m[1] + 2.0 * kx * ky * m[2] + ky * ky * m[3] +
+         ridge * (vx * vx + vy * vy);
+}
+
+__global__ __launch_bounds__(256) void k_velocity(const double* __restrict__ az, const double* __restrict__ y,
+                                                  const unsigned* __restrict__ amask,
+                                                  const long long* __restrict__ seg, double k, double ridge,
+                                                  double lx, double hx, double ly, double hy,
+                                                  double* __restrict__ out, double* __restrict__ resid,
+                                                  double* __restrict__ pred) {
+  __shared__ double sh[8];
+  __shared__ double mom[7];
+  __shared__ double sol[2];
+  const long f = blockIdx.x;
+  const long long b = seg[f], e = seg[f + 1];
+  double n = 0, cc = 0, cs = 0, ss = 0, cy = 0, sy = 0, yy = 0;
+  for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const double w = amask ? (double)__popc(amask[i]) : 1.0;
+    double s, c;
+    sincos(az[i], &s, &c);
+    const double yi = y[i];
+    n += w;
+    cc += w * c * c;
+    cs += w * c * s;
+    ss += w * s * s;
+    cy += w * c * yi;
+    sy += w * s * yi;
+    yy += w * yi * yi;
+  }
+  const double vals[7] = {n, cc, cs, ss, cy, sy, yy};
+  for (int v = 0; v < 7; ++v) {
+    const double r = block_sum(vals[v], sh);
+    if (threadIdx.x == 0) mom[v] = r;
+  }
+  if (threadIdx.x == 0) {
+    const double* m = mom;
+    const double H00 = k * k * m[1] + ridge, H01 = k * k * m[2], H11 = k * k * m[3] + ridge;
+    const double b0 = k * m[4], b1 = k * m[5];
+    const double det = H00 * H11 - H01 * H01;
+    double bx = 0.0, by = 0.0;
+    bool done = false;
+    if (det > 1e-300) {
+      const double vx = (H11 * b0 - H01 * b1) / det, vy = (H00 * b1 - H01 * b0) / det;
+      if (vx >= lx && vx <= hx && vy >= ly && vy <= hy) {
+        bx = vx;
+        by = vy;
+        done = true;
+      }
+    }
+    if (!done) {
+      double bc = INFINITY;
+      for (int edge = 0; edge < 4; ++edge) {
+        const int fix = edge >> 1;  // 0: vx fixed, 1: vy fixed
+        const double val = (fix == 0) ? ((edge & 1) ? hx : lx) : ((edge & 1) ? hy : ly);
+        double x;
+        if (fix == 0) {
+          x = H11 > 0 ? (b1 - H01 * val) / H11 : 0.0;
+          x = fmin(fmax(x, ly), hy);
+        } else {
+          x = H00 > 0 ? (b0 - H01 * val) / H00 : 0.0;
+          x = fmin(fmax(x, lx), hx);
+        }
+        const double vx = fix == 0 ? val : x, vy = fix == 0 ? x : val;
+        const double cst = qcost(vx, vy, k, ridge, m);
+        if (cst < bc) {
+          bc = cst;
+          bx = vx;
+          by = vy;
+        }
+      }
+    }
+    sol[0] = bx;
+    sol[1] = by;
+  }
+  __syncthreads();
+  const double vx = sol[0], vy = sol[1];
+  double r2 = 0.0, rmax = 0.0;
+  for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const double w = amask ? (double)__popc(amask[i]) : 1.0;
+    double s, c;
+    sincos(az[i], &s, &c);
+    const double pr = k * (vx * c + vy * s);
+    const double r = y[i] - pr;
+    r2 += w * r * r;
+    if (w > 0) rmax = fmax(rmax, fabs(r));
+    if (resid) resid[i] = r;
+    if (pred) pred[i] = pr;
+  }
+  const double R2 = block_sum(r2, sh);
+  const double RM = block_max(rmax, sh);
+  if (threadIdx.x == 0) {
+    double* o = out + f * 8;
+    o[0] = vx;
+    o[1] = vy;
+    o[2] = R2 + ridge * (vx * vx + vy * vy);               // cost at the optimum
+    o[3] = mom[0] > 0 ? sqrt(R2 / mom[0]) : 0.0;           // rmse (velocity_solver.py:283)
+    o[4] = RM;                                             // max |residual| (velocity_solver.py:284)
+    o[5] = mom[0];                                         // number of targets (with multiplicity)
+    o[6] = mom[1] * mom[3] - mom[2] * mom[2];              // normal-matrix determinant / k^4
+    o[7] = 0.0;
+  }
+}
+
+hipError_t launch_velocity(hipStream_t st, const double* az, const double* y, const unsigned* amask,
+                           const long long* seg, int F, double k, double ridge, const double* bounds4, double* out,
+                           double* resid, double* pred) {
+  if (F <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_velocity, dim3(F), dim3(256), 0, st, az, y, amask, seg, k, ridge, bounds4[0], bounds4[1],
+                     bounds4[2], bounds4[3], out, resid, pred);
+  return hipGetLastError();
+}
+
+}  // namespace rsl

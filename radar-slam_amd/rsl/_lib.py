@@ -1,0 +1,65 @@
+"""ctypes binding of librsl.so (C ABI declared in include/rsl.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C radar-slam_amd/csrc``) into
+``radar-slam_amd/lib/librsl.so``.  There is no fallback: if the library is missing, importing the
+product path raises ``ImportError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_longlong, c_void_p, c_char_p, POINTER
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get('RSL_LIBRARY', os.path.join(PKG_ROOT, 'lib', 'librsl.so'))
+
+RSL_OK, RSL_ERR_INVALID, RSL_ERR_UNSUPPORTED, RSL_ERR_HIP = 0, 1, 2, 3
+METHOD_BEAMFORMING, METHOD_MUSIC = 0, 1
+K_NAMES = ['range_fft', 'doppler_fft', 'detect', 'offsets', 'emit', 'doa_scan', 'cell_extras', 'confidence',
+           'velocity']
+
+_P = c_void_p
+# name -> (restype, argtypes); must mirror include/rsl.h (tests/test_abi.py checks both directions)
+SIGNATURES = {
+    'rsl_version': (c_int, []),
+    'rsl_create': (c_int, [POINTER(c_void_p), c_int]),
+    'rsl_destroy': (c_int, [_P]),
+    'rsl_last_error': (c_char_p, [_P]),
+    'rsl_set_stream': (c_int, [_P, _P]),
+    'rsl_sync': (c_int, [_P]),
+    'rsl_fft_supported': (c_int, [c_int]),
+    'rsl_timing_enable': (c_int, [_P, c_int]),
+    'rsl_timing_reset': (c_int, [_P]),
+    'rsl_timing_read': (c_int, [_P, c_int, POINTER(c_double), POINTER(c_longlong)]),
+    'rsl_rds': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
+    'rsl_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_int, c_int, _P, _P, _P]),
+    'rsl_peak_offsets': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P]),
+    'rsl_peak_emit': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_longlong, c_longlong,
+                              _P, _P, _P, _P, _P, _P, _P, _P]),
+    'rsl_steer_table_floats': (c_longlong, [c_int, c_int]),
+    'rsl_steer_table_build': (c_int, [POINTER(c_double), c_int, c_int, POINTER(c_float), POINTER(c_int)]),
+    'rsl_doa': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, _P, c_int, c_int, _P, _P, _P]),
+    'rsl_cell_extras': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, c_double, _P, _P, _P, _P,
+                                _P, _P]),
+    'rsl_confidence': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, c_longlong, _P, _P, _P, _P]),
+    'rsl_velocity': (c_int, [_P, _P, _P, _P, _P, c_int, c_double, c_double, POINTER(c_double), _P, _P, _P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load librsl.so once and declare every entry point's signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"librsl.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
+                          f"or `make -C radar-slam_amd/csrc` (there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,76 @@
+"""Parity comparators (CPU, numpy): explain every GPU/oracle difference by an fp32 near-tie of the
+reference's own fp64 values, or report it as unexplained.  Tolerances are stated here once:
+
+* RDS:      max |rds_gpu - rds_ref| <= RDS_ATOL_REL * max |rds_ref|           (c64 chain measured 1.6e-7)
+* peaks:    set equality, except cells whose reference decision margin is below PEAK_RTOL
+            (|p - max_neighbour| or |p - threshold| relative to p), which fp32 cannot resolve
+* DoA:      same grid index, or a different index whose reference |a^H s|^2 is within DOA_GTOL of the
+            reference maximum (near-tie / the +-90 deg alias); fraction of such cells reported
+* ESPRIT:   |deg_gpu - deg_ref| <= ESPRIT_TOL_DEG (= 1e-3 rad, the north-star DoA tolerance)
+* velocity: cost within VEL_COST_RTOL relative; (v_x, v_y) within VEL_ATOL m/s when well conditioned
+"""
+import numpy as np
+
+import radar_oracle as O
+
+RDS_ATOL_REL = 1e-5
+PEAK_RTOL = 2e-5
+DOA_GTOL = 2e-4
+ESPRIT_TOL_DEG = float(np.degrees(1e-3))
+VEL_COST_RTOL = 1e-6
+VEL_ATOL = 1e-4
+
+
+def rds_error(gpu, ref):
+    return float(np.abs(gpu - ref).max() / np.abs(ref).max())
+
+
+def _neighbour_max(p):
+    A, S, C = p.shape
+    pad = np.full((A, S + 2, C + 2), -np.inf)
+    pad[:, 1:-1, 1:-1] = p
+    m = np.full(p.shape, -np.inf)
+    for di in (-1, 0, 1):
+        for dj in (-1, 0, 1):
+            if di == 0 and dj == 0:
+                continue
+            m = np.maximum(m, pad[:, 1 + di:1 + di + S, 1 + dj:1 + dj + C])
+    return m
+
+
+def peak_diff(gpu_mask, ref_rds, *, threshold_db=-20.0, gate=(0, 1 << 30)):
+    """gpu_mask bool [A, S, C].  Returns (n_gpu, n_ref, n_diff, n_unexplained)."""
+    ref_mask, _ = O.peak_mask(ref_rds, threshold_db)
+    A, S, C = ref_rds.shape
+    g = np.zeros(S, bool)
+    g[max(gate[0], 0):min(gate[1], S - 1) + 1] = True
+    ref_mask &= g[None, :, None]
+    diff = gpu_mask ^ ref_mask
+    p = np.abs(ref_rds) ** 2
+    nb = _neighbour_max(p)
+    thr = 10 ** (threshold_db / 10) - 1e-12
+    near_max = np.abs(p - nb) <= PEAK_RTOL * np.maximum(p, nb)
+    near_thr = np.abs(p - thr) <= PEAK_RTOL * thr
+    unexpl = diff & ~(near_max | near_thr)
+    return int(gpu_mask.sum()), int(ref_mask.sum()), int(diff.sum()), int(unexpl.sum())
+
+
+def doa_diff(gpu_idx, ref_sigs, steer, method='music'):
+    """gpu_idx [N] grid indices; ref_sigs c128 [N, M] (unit norm, from the fp64 reference RDS)."""
+    g = np.abs(ref_sigs @ steer.conj().T) ** 2
+    if method == 'music':
+        spec = O.music_spectrum_closed(ref_sigs, steer)
+        ref_idx = np.argmax(spec, axis=1)
+    else:
+        ref_idx = np.argmax(g, axis=1)
+    n = np.arange(len(gpu_idx))
+    mism = gpu_idx != ref_idx
+    explained = g[n, gpu_idx] >= g[n, ref_idx] - DOA_GTOL
+    return int(mism.sum()), int((mism & ~explained).sum()), ref_idx
+
+
+def esprit_diff(gpu_deg, ref_deg):
+    both_nan = np.isnan(gpu_deg) & np.isnan(ref_deg)
+    d = np.abs(gpu_deg - ref_deg)
+    d[both_nan] = 0
+    return float(np.nanmax(d) if d.size else 0.0), int((np.isnan(gpu_deg) != np.isnan(ref_deg)).sum())

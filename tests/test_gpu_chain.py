@@ -1,0 +1,129 @@
+"""GPU parity of the batched chain (librsl via rsl.RadarChain) against the oracle, on identical seeded cubes.
+
+Cubes come from the oracle's restatement of simulate_raw.synthesize_frame (bit-identical to the
+reference, pinned in test_oracle_golden.py) and are fed to the GPU as complex64.
+"""
+import numpy as np
+import pytest
+
+import parity as P
+import radar_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {  # name: (A, C, T_c)
+    'tiny': (8, 16, 3.2e-6),
+    'odd400': (8, 16, 40e-6),
+    'cfg1': (8, 64, 25.6e-6),
+    'cfg2': (8, 128, 51.2e-6),
+    'cfg5a16': (16, 32, 12.8e-6),
+}
+
+
+def make_frames(A, C, Tc, F, seed0):
+    frames = []
+    for f in range(F):
+        np.random.seed(seed0 + f)
+        frames.append(O.synthesize_frame(O.TEST_SCENE, chirp_duration=Tc, num_chirps=C, num_antennas=A))
+    return np.stack(frames)
+
+
+@pytest.fixture(scope='module')
+def runs(ctx):
+    import rsl
+    out = {}
+    for name, (A, C, Tc) in CFGS.items():
+        F = 2
+        frames = make_frames(A, C, Tc, F, 1000)
+        cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
+        ch = rsl.RadarChain(cfg, F, ctx)
+        cube = ctx.to_dev(frames.astype(np.complex64))
+        ch.run(cube)
+        res = ch.results()
+        res['rds'] = ch.rds.cpu().numpy()
+        res['mask_words'] = ch.mask.cpu().numpy()
+        res['frames'] = frames
+        res['cfg'] = cfg
+        res['chain'] = ch
+        out[name] = res
+    return out
+
+
+@pytest.mark.parametrize('name', list(CFGS))
+def test_rds_parity(runs, name):
+    r = runs[name]
+    for f in range(len(r['frames'])):
+        ref = O.range_doppler_spectrum(r['frames'][f], chirp_duration=r['cfg'].chirp_duration)
+        err = P.rds_error(r['rds'][f], ref)
+        assert err <= P.RDS_ATOL_REL, (name, f, err)
+
+
+def _mask_bool(words, C):
+    A, S, W = words.shape
+    bits = np.unpackbits(words.view(np.uint8).reshape(A, S, W, 8), axis=-1, bitorder='little')
+    return bits.reshape(A, S, W * 64)[:, :, :C].astype(bool)
+
+
+@pytest.mark.parametrize('name', list(CFGS))
+def test_peaks_parity(runs, name):
+    r = runs[name]
+    cfg = r['cfg']
+    ch = r['chain']
+    for f in range(len(r['frames'])):
+        ref = O.range_doppler_spectrum(r['frames'][f], chirp_duration=cfg.chirp_duration)
+        gm = _mask_bool(r['mask_words'][f], cfg.num_chirps)
+        ng, nr, nd, nu = P.peak_diff(gm, ref, gate=(ch.i_lo, ch.i_hi))
+        assert nu == 0, (name, f, ng, nr, nd, nu)
+        assert nd <= max(2, 1e-4 * nr), (name, f, nd, nr)
+        # entry list order/contents == oracle order (antenna -> range -> doppler)
+        a, i, j, db = O.peak_arrays(ref)
+        eb = r['entry_base']
+        ga, gi, gj = (r['e_ant'][eb[f]:eb[f + 1]], r['e_rbin'][eb[f]:eb[f + 1]], r['e_dbin'][eb[f]:eb[f + 1]])
+        if nd == 0:
+            assert (ga == a).all() and (gi == i).all() and (gj == j).all()
+            assert np.abs(r['e_pdb'][eb[f]:eb[f + 1]] - db).max() < 1e-4
+
+
+@pytest.mark.parametrize('name', list(CFGS))
+def test_doa_esprit_parity(runs, name):
+    r = runs[name]
+    cfg = r['cfg']
+    A = cfg.num_antennas
+    lam = 3e8 / cfg.fc
+    steer = O.steering_matrix(O.azimuth_grid(), A)
+    cb = r['cell_base']
+    tot_m = tot_u = 0
+    for f in range(len(r['frames'])):
+        ref = O.range_doppler_spectrum(r['frames'][f], chirp_duration=cfg.chirp_duration)
+        sl = slice(cb[f], cb[f + 1])
+        rc = r['c_rc'][sl]
+        ii, jj = rc // cfg.num_chirps, rc % cfg.num_chirps
+        sigs = np.stack([O.spatial_signature(ref, i, j) for i, j in zip(ii, jj)]) if len(rc) else np.zeros((0, A))
+        nm, nu, ref_idx = P.doa_diff(r['gidx'][sl], sigs, steer, 'music')
+        tot_m += nm
+        tot_u += nu
+        e_ref = O.esprit_closed(sigs)
+        emax, nnan = P.esprit_diff(r['esprit'][sl], e_ref)
+        assert nnan == 0 and emax <= P.ESPRIT_TOL_DEG, (name, f, emax, nnan)
+        ph = O.observed_phase(sigs)
+        dph = np.angle(np.exp(1j * (r['phase'][sl] - ph)))
+        assert np.abs(dph).max() < 1e-4
+    assert tot_u == 0, (name, tot_m, tot_u)
+
+
+@pytest.mark.parametrize('name', list(CFGS))
+def test_velocity_parity(runs, name):
+    r = runs[name]
+    cfg = r['cfg']
+    cb = r['cell_base']
+    grid = r['grid']
+    for f in range(len(r['frames'])):
+        sl = slice(cb[f], cb[f + 1])
+        w = np.array([bin(int(m) & 0xffffffff).count('1') for m in r['c_amask'][sl]])
+        az = np.repeat(np.radians(grid[r['gidx'][sl]]), w)
+        y = np.repeat(r['phase'][sl], w)
+        vx, vy, cost = O.velocity_ls(az, y, lambda_c=3e8 / cfg.fc)
+        v = r['velocity'][f]
+        assert abs(v[2] - cost) <= P.VEL_COST_RTOL * cost
+        assert abs(v[0] - vx) < P.VEL_ATOL and abs(v[1] - vy) < P.VEL_ATOL
+        assert int(v[5]) == len(y)
