@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: radar frames/s end-to-end on 8ch x 128chirp x 512 cubes (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W --frames-per-step F]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = one pass of the full per-frame chain (configs[2]: RDS + peak detection + MUSIC DoA argmax +
+ESPRIT + least-squares velocity) over a batch of F synthetic frames already resident in HBM.  Frames
+shard across ranks (one process per GPU, weak scaling, no data-path collective); per step the per-frame
+velocities are gathered to rank 0 over RCCL (the trajectory reduction of the north star).  Rank 0
+prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'radar-slam_amd'))
+
+METRIC = "radar frames/sec end-to-end, 8ch×128chirp×512 cube; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+SCENE = [  # tests/test_synth_raw.py:165-190 (reference)
+    (20.0, 0.0, -10.0, 0.0), (40.0, math.radians(45.0), -8.0, 5.0), (60.0, math.radians(-30.0), -12.0, -3.0)]
+
+
+def target_pattern(A, S, fc=77e9, B=1e9, Tc=51.2e-6):
+    """Noise-free scatterer response [A, S] of simulate_raw.synthesize_frame (simulate_raw.py:102-209):
+    independent of the chirp index, so one pattern serves every chirp of every frame."""
+    c = 3e8
+    lam = c / fc
+    pos = np.arange(A) * lam / 2
+    t = np.linspace(0, Tc, S)
+    k = B / Tc
+    chirp = lambda tt: np.exp(1j * 2 * np.pi * (fc * tt + 0.5 * k * tt ** 2))
+    ref = chirp(t)
+    out = np.zeros((A, S), complex)
+    for r, az, rcs, vr in SCENE:
+        amp = np.sqrt(10 ** (rcs / 10)) / (4 * np.pi * r ** 2)
+        ph = amp * np.exp(1j * (4 * np.pi * vr * fc / c + 2 * np.pi * pos * np.sin(az) / lam))
+        td = t - 2 * r / c
+        v = (td >= 0) & (td <= Tc)
+        out[:, v] += ph[:, None] * (chirp(td[v]) * np.conj(ref[v]))[None, :]
+    return out
+
+
+def make_cubes(torch, dev, nb, F, A, C, S, seed):
+    pat = torch.from_numpy(target_pattern(A, S).astype(np.complex64)).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    cubes = []
+    sig = math.sqrt(0.01)  # noise_power 0.01 (simulate_raw.py:216-218)
+    for _ in range(nb):
+        x = torch.randn((F, A, C, S, 2), device=dev, generator=g, dtype=torch.float32).mul_(sig)
+        z = torch.view_as_complex(x)
+        z += pat[None, :, None, :]
+        cubes.append(z)
+    return cubes
+
+
+def cpu_baseline(budget_s=20.0):
+    """Oracle ('port') chain timed on one host core over a bounded sample of one cfg2 frame:
+    loop-faithful RDS (dechirp.py:196-211), peaks (dechirp.py:215-278), per-peak eigh MUSIC
+    (angle_estimation.py:109-176) and SVD ESPRIT (angle_estimation.py:178-225) on a sample of peaks,
+    exact LS velocity; per-frame time = stage times, peak stages scaled by N_p / sample."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import radar_oracle as O
+    os.environ.setdefault('OMP_NUM_THREADS', '1')
+    np.random.seed(1000)
+    Tc = 51.2e-6
+    frame = O.synthesize_frame(O.TEST_SCENE, chirp_duration=Tc, num_chirps=128, num_antennas=8)
+    t0 = time.perf_counter()
+    rds = O.range_doppler_spectrum_loop(frame, chirp_duration=Tc)
+    t_rds = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    pk = O.extract_peaks(rds)
+    t_pk = time.perf_counter() - t0
+    peaks = pk['peaks']
+    grid = O.azimuth_grid()
+    t_music = t_esp = 0.0
+    n = 0
+    t_start = time.perf_counter()
+    sigs = []
+    while n < len(peaks) and time.perf_counter() - t_start < budget_s:
+        p = peaks[n]
+        s = O.spatial_signature(rds, p['range_bin'], p['doppler_bin'])
+        t0 = time.perf_counter()
+        spec = O.music_spectrum_eigh(s, grid)
+        grid[np.argmax(spec)]
+        t1 = time.perf_counter()
+        O.esprit_svd(s)
+        t2 = time.perf_counter()
+        t_music += t1 - t0
+        t_esp += t2 - t1
+        sigs.append(s)
+        n += 1
+    Np = len(peaks)
+    sigs = np.array(sigs)
+    t0 = time.perf_counter()
+    O.velocity_ls(np.radians(grid[np.zeros(len(sigs), int)]), O.observed_phase(sigs), lambda_c=3e8 / 77e9)
+    t_vel = (time.perf_counter() - t0) * Np / max(n, 1)
+    per_frame = t_rds + t_pk + (t_music + t_esp) * Np / max(n, 1) + t_vel
+    return dict(value=1.0 / per_frame, unit="frames/s", cores=1, kind="port",
+                sample=f"1 cfg2 frame (8x128x512): loop-faithful RDS {t_rds:.3f}s + peaks {t_pk:.3f}s (N_p={Np}) + "
+                       f"eigh-MUSIC/SVD-ESPRIT on {n} of {Np} peaks ({(t_music + t_esp) / max(n, 1) * 1e3:.2f} ms/peak, "
+                       f"scaled to N_p) + LS velocity; oracle/radar_oracle.py on 1 host core")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--frames-per-step', type=int, default=1000)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-budget', type=float, default=20.0)
+    ap.add_argument('--no-timing', action='store_true', help='disable per-kernel hipEvent timing')
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    import rsl
+    A, C, S, F = 8, 128, 512, args.frames_per_step
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=51.2e-6)
+    ctx = rsl.get_context(local)
+    chain = rsl.RadarChain(cfg, F, ctx)
+    nb = 2
+    cubes = make_cubes(torch, dev, nb, F, A, C, S, seed=1234 + 7919 * rank)
+    gather_buf = [torch.empty((F, 2), dtype=torch.float64, device=dev) for _ in range(world)] if world > 1 else None
+
+    def step(i):
+        chain.run(cubes[i % nb])
+        if world > 1:  # trajectory reduction: per-frame (vx, vy) to every rank over RCCL/xGMI
+            dist.all_gather(gather_buf, chain.vel[:, :2].contiguous())
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ne, nc = chain.totals()
+    if ne > chain.entry_cap or nc > chain.cell_cap:
+        raise RuntimeError('peak capacity exceeded')
+    if not args.no_timing:
+        ctx.timing(True)
+        ctx.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = ctx.timing_read() if not args.no_timing else {}
+    ctx.timing(False)
+    ne, nc = chain.totals()
+    frames_total = F * args.steps * world
+    fps = frames_total / elapsed
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    G = len(chain.grid)
+    line = {
+        "metric": METRIC, "value": fps, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "configs[2]: 8ch x 128chirp x 512 synthetic cube, full chain "
+                               "(RDS + peaks + MUSIC argmax + ESPRIT + LS velocity)",
+                   "frames_per_step": F, "frames_per_gpu_per_step": F, "antennas": A, "chirps": C, "samples": S,
+                   "doa_grid": G, "parallelism": f"frame-sharded x{world}"},
+        "peaks_per_frame": ne / F, "cells_per_frame": nc / F,
+    }
+    if kt:
+        ms_doa, n_doa = kt['doa_scan']
+        flops = nc * G * (8 * A + 5)               # per launch: unique cells x grid x (8M + 5)
+        t_doa = ms_doa / max(n_doa, 1) * 1e-3
+        ach = flops / t_doa / 1e12
+        line["roofline"] = {"bound": "mfma", "kernel": "k_doa_scan", "achieved": ach, "peak": FP32_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": ach / FP32_PEAK_TFLOPS, "traffic": None,
+                            "avg_launch_ms": ms_doa / max(n_doa, 1),
+                            "algorithmic_flops_per_launch": flops}
+        t_fft = (kt['range_fft'][0] + kt['doppler_fft'][0]) / max(kt['range_fft'][1], 1) * 1e-3
+        fft_bytes = 2 * A * C * S * 8 * F
+        line["fft_stage"] = {"bound": "hbm", "achieved": fft_bytes / t_fft / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": fft_bytes / t_fft / 1e9 / HBM_PEAK_GBS,
+                             "algorithmic_bytes_per_launch": fft_bytes}
+        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) for k, v in kt.items() if v[1]}
+    if not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        except Exception as e:  # the baseline is reported, never the target
+            line["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
