@@ -38,7 +38,8 @@ extern "C" {
 #define RSL_K_CELL_EXTRAS 6
 #define RSL_K_CONFIDENCE 7
 #define RSL_K_VELOCITY 8
-#define RSL_K_COUNT 9
+#define RSL_K_AUX 9
+#define RSL_K_COUNT 10
 
 typedef struct rsl_context* rsl_handle;
 
@@ -48,6 +49,7 @@ int rsl_destroy(rsl_handle h);
 const char* rsl_last_error(rsl_handle h);
 int rsl_set_stream(rsl_handle h, void* hip_stream); /* NULL = null stream */
 int rsl_sync(rsl_handle h);
+/* 1 = radix-{2,3,4,5,7,8} LDS FFT, 2 = direct-DFT fallback (any n <= 4096), 0 = unsupported */
 int rsl_fft_supported(int n);
 
 /* Per-kernel device time (hipEvents recorded on the handle's stream around every launch). */
@@ -125,6 +127,23 @@ int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const voi
  *     out f64 [F, 8] = {vx, vy, cost, rmse, max_residual, n, det, 0}; resid/pred f64 [N] nullable. */
 int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask, const void* seg, int F, double k,
                  double ridge, const double* bounds4, void* out, void* resid, void* pred);
+
+/* a3-a6  SignalPreprocessor.dechirp_signal / apply_window / remove_dc / process_chirp (dechirp.py:85-166):
+ *     out[r, s] = in[r, s] * table[s], then (dc != 0) minus the row's complex mean.  in/out c64 [rows, S]. */
+int rsl_preprocess_rows(rsl_handle h, const void* in, long long rows, int S, const void* table, int dc, void* out);
+
+/* a25, a27  compute_phase_difference_model + cost_function (velocity_solver.py:65-176), general 6-DoF:
+ *     pred = k (v + w x p).d, d = (cos el cos az, cos el sin az, sin el); pos f64 [n,3], ang f64 [n,2],
+ *     x f64 [6] = (v, w) (device); y f64 [n] nullable; wrap != 0 wraps residuals to (-pi, pi]
+ *     (velocity_solver_improved.py:255); cost f64 [1] = sum r^2 + ridge |x|^2 (nullable). */
+int rsl_phase_model(rsl_handle h, const void* pos, const void* ang, long long n, const void* x, double k,
+                    const void* y, int wrap, double ridge, void* pred, void* resid, void* cost);
+
+/* a28  two_step_optimization (velocity_solver.py:178-307) for arbitrary (pos, ang): exact box-constrained
+ *     linear least squares over nv = 3 (v, w = 0) or 6 (v, w) unknowns (BVLS active set, fp64).
+ *     lo/hi f64 [nv] device bounds; out f64 [nv + 1] = x, cost. */
+int rsl_bvls(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int nv,
+             double ridge, const void* lo, const void* hi, void* out);
 
 #ifdef __cplusplus
 }

@@ -99,13 +99,14 @@ extern "C" {
 
 int rsl_version(void) { return 1; }
 
+// 1: radix-{2,3,4,5,7,8} Stockham FFT in LDS; 2: any other length up to 4096 (direct DFT fallback); 0: no.
 int rsl_fft_supported(int n) {
   switch (n) {
     case 8: case 16: case 32: case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096:
     case 25: case 50: case 100: case 200: case 400: case 800: case 1600:
       return 1;
     default:
-      return 0;
+      return (n >= 1 && n <= 4096) ? 2 : 0;
   }
 }
 
@@ -360,6 +361,38 @@ int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask,
                                         (const long long*)seg, F, k, ridge, bounds4, (double*)out, (double*)resid,
                                         (double*)pred),
                    "velocity");
+}
+
+int rsl_preprocess_rows(rsl_handle h, const void* in, long long rows, int S, const void* table, int dc, void* out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (rows < 0 || S <= 0 || !in || !table || !out) return fail(h, RSL_ERR_INVALID, "rsl_preprocess_rows: bad argument");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h, rsl::launch_preprocess_rows(h->stream, (const float2*)in, rows, S, (const float2*)table, dc,
+                                                  (float2*)out),
+                   "preprocess_rows");
+}
+
+int rsl_phase_model(rsl_handle h, const void* pos, const void* ang, long long n, const void* x, double k,
+                    const void* y, int wrap, double ridge, void* pred, void* resid, void* cost) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 0 || !pos || !ang || !x) return fail(h, RSL_ERR_INVALID, "rsl_phase_model: bad argument");
+  if ((resid || cost) && !y) return fail(h, RSL_ERR_INVALID, "rsl_phase_model: residual/cost need y");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h, rsl::launch_phase_model(h->stream, (const double*)pos, (const double*)ang, n, (const double*)x,
+                                              k, (const double*)y, wrap, ridge, (double*)pred, (double*)resid,
+                                              (double*)cost),
+                   "phase_model");
+}
+
+int rsl_bvls(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int nv,
+             double ridge, const void* lo, const void* hi, void* out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 0 || (nv != 3 && nv != 6) || !pos || !ang || !y || !lo || !hi || !out || ridge < 0)
+    return fail(h, RSL_ERR_INVALID, "rsl_bvls: bad argument");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h, rsl::launch_bvls(h->stream, (const double*)pos, (const double*)ang, n, (const double*)y, k, nv,
+                                       ridge, (const double*)lo, (const double*)hi, (double*)out),
+                   "bvls");
 }
 
 }  // extern "C"

@@ -142,6 +142,86 @@ static hipError_t launch_k2(hipStream_t st, const float2* work, int F, int A, in
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Any-length fallback (sizes whose prime factors are not all in {2,3,5,7}, e.g. a chirp_subset of 59
+// chirps): direct DFT from LDS with the fp64-accurate twiddle table, O(N) per output point.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_range_dft(const float2* __restrict__ cube, int Ct, int c0, int C, int S,
+                                                        const float2* __restrict__ table,
+                                                        const float2* __restrict__ tw, int dc,
+                                                        float2* __restrict__ work) {
+  extern __shared__ float2 sm[];
+  float2* tws = sm;
+  float2* row = sm + S;
+  const long r = blockIdx.x;  // (f*A + a)*C + c
+  const long fa = r / C;
+  const int c = (int)(r - fa * C);
+  const float2* src = cube + ((size_t)fa * Ct + c0 + c) * S;
+  for (int k = threadIdx.x; k < S; k += kThreads) {
+    tws[k] = tw[k];
+    row[k] = cmul(src[k], table[k]);
+  }
+  __syncthreads();
+  float2* dst = work + (size_t)r * S;
+  for (int k = threadIdx.x; k < S; k += kThreads) {
+    float2 acc = make_float2(0.f, 0.f);
+    int idx = 0;
+    for (int n = 0; n < S; ++n) {
+      acc = cadd(acc, cmul(row[n], tws[idx]));
+      idx += k;
+      if (idx >= S) idx -= S;
+    }
+    dst[k] = (dc && k == 0) ? make_float2(0.f, 0.f) : acc;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_doppler_dft(const float2* __restrict__ work, int C, int S,
+                                                          const float2* __restrict__ tw, float2* __restrict__ rds) {
+  extern __shared__ float2 sm[];
+  float2* tws = sm;
+  float2* col = sm + C;
+  const long r = blockIdx.x;  // (f*A + a)*S + k
+  const long fa = r / S;
+  const int k = (int)(r - fa * S);
+  const float2* src = work + (size_t)fa * C * S + k;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    tws[c] = tw[c];
+    col[c] = src[(size_t)c * S];
+  }
+  __syncthreads();
+  int i = k + S / 2;
+  if (i >= S) i -= S;
+  float2* dst = rds + ((size_t)fa * S + i) * C;
+  for (int j = threadIdx.x; j < C; j += kThreads) {
+    int d = j - C / 2;
+    if (d < 0) d += C;
+    float2 acc = make_float2(0.f, 0.f);
+    int idx = 0;
+    for (int n = 0; n < C; ++n) {
+      acc = cadd(acc, cmul(col[n], tws[idx]));
+      idx += d;
+      if (idx >= C) idx -= C;
+    }
+    dst[j] = acc;
+  }
+}
+
+hipError_t launch_range_dft(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
+                            const float2* table, const float2* tw, int dc, float2* work) {
+  const long nblk = (long)F * A * C;
+  hipLaunchKernelGGL(k_range_dft, dim3((unsigned)nblk), dim3(kThreads), sizeof(float2) * 2 * (size_t)S, st, cube, Ct,
+                     c0, C, S, table, tw, dc, work);
+  return hipGetLastError();
+}
+
+hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw,
+                              float2* rds) {
+  const long nblk = (long)F * A * S;
+  hipLaunchKernelGGL(k_doppler_dft, dim3((unsigned)nblk), dim3(kThreads), sizeof(float2) * 2 * (size_t)C, st, work, C,
+                     S, tw, rds);
+  return hipGetLastError();
+}
+
 #define RSL_FFT_SIZES(X) \
   X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048) X(4096) X(25) X(50) X(100) X(200) X(400) X(800) X(1600)
 
@@ -156,8 +236,11 @@ hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, in
     RSL_FFT_SIZES(CASE)
 #undef CASE
     default:
-      *supported = false;
-      return hipSuccess;
+      if (S > 4096) {
+        *supported = false;
+        return hipSuccess;
+      }
+      return launch_range_dft(st, cube, F, A, Ct, chirp0, C, S, table, tw_S, dc, work);
   }
 }
 
@@ -172,8 +255,11 @@ hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, 
     RSL_FFT_SIZES(CASE)
 #undef CASE
     default:
-      *supported = false;
-      return hipSuccess;
+      if (C > 4096) {
+        *supported = false;
+        return hipSuccess;
+      }
+      return launch_doppler_dft(st, work, F, A, C, S, tw_C, rds);
   }
 }
 

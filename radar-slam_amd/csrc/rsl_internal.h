@@ -47,3 +47,12 @@ hipError_t launch_velocity(hipStream_t st, const double* az, const double* y, co
                            double* resid, double* pred);
 
 }  // namespace rsl
+
+namespace rsl {
+hipError_t launch_preprocess_rows(hipStream_t st, const float2* in, long rows, int S, const float2* table, int dc,
+                                  float2* out);
+hipError_t launch_phase_model(hipStream_t st, const double* pos, const double* ang, long n, const double* x, double k,
+                              const double* y, int wrap, double ridge, double* pred, double* resid, double* cost);
+hipError_t launch_bvls(hipStream_t st, const double* pos, const double* ang, long n, const double* y, double k, int nv,
+                       double ridge, const double* lo, const double* hi, double* out);
+}  // namespace rsl

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get('RSL_LIBRARY', os.path.join(PKG_ROOT, 'lib', 'librsl.s
 RSL_OK, RSL_ERR_INVALID, RSL_ERR_UNSUPPORTED, RSL_ERR_HIP = 0, 1, 2, 3
 METHOD_BEAMFORMING, METHOD_MUSIC = 0, 1
 K_NAMES = ['range_fft', 'doppler_fft', 'detect', 'offsets', 'emit', 'doa_scan', 'cell_extras', 'confidence',
-           'velocity']
+           'velocity', 'aux']
 
 _P = c_void_p
 # name -> (restype, argtypes); must mirror include/rsl.h (tests/test_abi.py checks both directions)
@@ -43,6 +43,9 @@ SIGNATURES = {
                                 _P, _P]),
     'rsl_confidence': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, c_longlong, _P, _P, _P, _P]),
     'rsl_velocity': (c_int, [_P, _P, _P, _P, _P, c_int, c_double, c_double, POINTER(c_double), _P, _P, _P]),
+    'rsl_preprocess_rows': (c_int, [_P, _P, c_longlong, c_int, _P, c_int, _P]),
+    'rsl_phase_model': (c_int, [_P, _P, _P, c_longlong, _P, c_double, _P, c_int, c_double, _P, _P, _P]),
+    'rsl_bvls': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, _P, _P, _P]),
 }
 
 _lib = None

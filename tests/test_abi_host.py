@@ -1,0 +1,184 @@
+"""CPU: the C-ABI library loads and exports exactly the symbols include/rsl.h declares; host-side helpers
+(fp64 tables, steering operand layout, range gate) and the drop-in module surface (names, parameters,
+defaults) match the reference."""
+import ast
+import ctypes
+import inspect
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import radar_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'rsl.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'^\s*(?:[a-z_ ]+\*?\s+)?\**(rsl_[a-z0-9_]+)\s*\(', src, flags=re.M)))
+
+
+def test_library_exports_header():
+    import rsl
+    from rsl import _lib
+    lib = rsl.load()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f'{n} declared in rsl.h but not exported'
+    assert sorted(_lib.SIGNATURES) == names, 'ctypes signature table out of sync with rsl.h'
+    assert lib.rsl_version() == 1
+
+
+def test_fft_support_table():
+    import rsl
+    lib = rsl.load()
+    for n in (8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 25, 50, 100, 200, 400, 800, 1600):
+        assert lib.rsl_fft_supported(n) == 1
+    for n in (1, 3, 11, 13, 59, 300, 4095):
+        assert lib.rsl_fft_supported(n) == 2
+    for n in (0, -4, 4097, 8192):
+        assert lib.rsl_fft_supported(n) == 0
+
+
+def test_null_handle_errors():
+    import rsl
+    lib = rsl.load()
+    assert lib.rsl_sync(None) == 1
+    assert lib.rsl_rds(None, None, 1, 8, 64, 0, 64, 256, None, 1, None, None) == 1
+    assert lib.rsl_last_error(None) == b'null handle'
+
+
+def test_steer_table_layout():
+    """MFMA A-operand layout (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][4s + (l>>4)]) built by the
+    library's host helper equals a direct construction from the [Re; Im] stacked steering rows."""
+    import rsl
+    lib = rsl.load()
+    G, M = 361, 8
+    grid = O.azimuth_grid()
+    st = O.steering_matrix(grid, M)
+    n = lib.rsl_steer_table_floats(G, M)
+    out = np.zeros(n, np.float32)
+    nt = ctypes.c_int()
+    flat = np.ascontiguousarray(st).view(np.float64)
+    rc = lib.rsl_steer_table_build(flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), G, M,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(nt))
+    assert rc == 0 and nt.value == (2 * G + 15) // 16
+    rows = np.zeros((nt.value * 16, 2 * M))
+    rows[0:2 * G:2] = np.concatenate([st.real, st.imag], axis=1)
+    rows[1:2 * G:2] = np.concatenate([-st.imag, st.real], axis=1)
+    tab = out.reshape(nt.value, 1, 64, 4)
+    for t in range(nt.value):
+        for lane in range(64):
+            for s in range(4):
+                assert tab[t, 0, lane, s] == np.float32(rows[16 * t + (lane & 15), 4 * s + (lane >> 4)])
+    # the real GEMM on these rows reproduces |a^H s|^2
+    rs = np.random.RandomState(0)
+    s = rs.randn(5, M) + 1j * rs.randn(5, M)
+    S = np.concatenate([s.real, s.imag], axis=1).T
+    D = rows[:2 * G] @ S
+    g = D[0::2] ** 2 + D[1::2] ** 2
+    assert np.allclose(g.T, np.abs(s @ st.conj().T) ** 2)
+
+
+def test_host_tables_match_oracle():
+    from rsl import tables
+    for Tc in (3.2e-6, 25.6e-6, 40e-6, 51.2e-6):
+        S = tables.samples_per_chirp(Tc, 10e6)
+        ref = O.reference_chirp(77e9, 1e9, Tc, 10e6)
+        assert np.array_equal(tables.reference_chirp(77e9, 1e9, Tc, 10e6), ref)
+        t = tables.chirp_table(77e9, 1e9, Tc, 10e6, 'hann', S)
+        assert np.array_equal(t, np.conj(ref) * O.window('hann', S))
+        i_lo, i_hi = tables.range_gate(1e9, S, 1.0, 200.0)
+        r = O.range_axis(1e9, S)
+        ok = (r >= 1.0) & (r <= 200.0)
+        assert ok[i_lo:i_hi + 1].all() and ok.sum() == i_hi - i_lo + 1
+    with pytest.raises(ValueError):
+        tables.chirp_table(77e9, 1e9, 40e-6, 10e6, 'hann', 256)
+    with pytest.raises(ValueError):
+        tables.window_values('kaiser', 16)
+    assert np.array_equal(tables.azimuth_grid(), O.azimuth_grid())
+    st = tables.steering_matrix(O.azimuth_grid(), np.arange(8) * (3e8 / 77e9 / 2), 3e8 / 77e9)
+    assert np.array_equal(st, O.steering_matrix(O.azimuth_grid(), 8))
+    # threshold: p + 1e-12 > 10^(thr/10)  <=>  p > thr_p
+    thr = tables.power_threshold(-20.0)
+    for p in (0.0099999, 0.01, 0.0100001):
+        assert (p > thr) == (10 * np.log10(p + 1e-12) > -20.0)
+
+
+def _norm_default(v):
+    if v is None:
+        return None
+    try:
+        return repr(ast.literal_eval(v))
+    except Exception:
+        return v.replace(' ', '')
+
+
+def _norm_obj(d):
+    if d is inspect.Parameter.empty:
+        return None
+    if isinstance(d, np.ndarray):
+        return f"np.array({d.tolist()})".replace(' ', '')
+    return repr(d)
+
+
+def test_dropin_surface_matches_reference():
+    import importlib
+    ref = json.load(open(os.path.join(ROOT, 'tests', 'golden', 'ref_signatures.json')))
+    for mod, members in ref.items():
+        m = importlib.import_module(mod)
+        for name, spec in members.items():
+            obj = getattr(m, name)
+            if isinstance(spec, dict):
+                for meth, params in spec.items():
+                    sig = inspect.signature(getattr(obj, meth))
+                    got = [[p.name, _norm_obj(p.default)] for p in sig.parameters.values()]
+                    want = [[n, _norm_default(d)] for n, d in params]
+                    if meth != '__init__' or name != 'PoseIntegrator':
+                        assert got == want, (mod, name, meth, got, want)
+                    else:
+                        assert [g[0] for g in got] == [w[0] for w in want]
+            else:
+                sig = inspect.signature(obj)
+                got = [[p.name, _norm_obj(p.default)] for p in sig.parameters.values()]
+                want = [[n, _norm_default(d)] for n, d in spec]
+                assert got == want, (mod, name, got, want)
+
+
+def test_pose_integration_dropin(golden):
+    from src.pose_integration.pose_integration import PoseIntegrator
+    z = golden('pose')
+    p = PoseIntegrator()
+    assert np.array_equal(p.integrate_translational_velocity(z['vel'], z['ts']), z['positions'])
+    ori, rot = p.integrate_angular_velocity(z['om'], z['ts'])
+    assert np.abs(ori - z['orientations']).max() < 1e-12 and np.abs(rot - z['rotations']).max() < 1e-12
+    pe = PoseIntegrator(integration_method='euler', smoothing=False)
+    assert np.array_equal(pe.integrate_translational_velocity(z['vel'], z['ts']), z['positions_euler'])
+    with pytest.raises(ValueError, match='broadcast'):
+        p.integrate_pose(z['vel'], z['om'], z['ts'])
+    one = p.integrate_pose(z['vel'][:1], z['om'][:1], z['ts'][:1])
+    assert one['total_rotation'] == float(z['one_total_rotation'])
+
+
+def test_product_path_has_no_oracle_import():
+    """The product package never imports the oracle (test infrastructure only)."""
+    pkg = os.path.join(ROOT, 'radar-slam_amd')
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith('.py'):
+                txt = open(os.path.join(dp, f)).read()
+                assert 'radar_oracle' not in txt and "'oracle'" not in txt, f
+
+
+def test_context_requires_device():
+    import torch
+    import rsl
+    if torch.cuda.is_available():
+        pytest.skip('device present')
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        rsl.Context(0)
