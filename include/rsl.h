@@ -121,12 +121,14 @@ int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const voi
                    long long n, const void* gidx, const void* steer_c128, const void* steer_phase, void* conf);
 
 /* a25-a29  VelocitySolver.two_step_optimization / solve_velocity (velocity_solver.py:65-355): exact
- *     box-constrained LS for (v_x, v_y) per segment (segments = frames).  az f64 [N] radians, y f64 [N]
+ *     box-constrained LS for (v_x, v_y) per segment (segments = frames).  az f64 [N] radians, or (when gidx
+ *     i32 [N] is non-null) az = az_table[gidx] with az_table f64 [G], G <= 2048; y f64 [N]
  *     observed phase, amask u32 [N] (nullable; multiplicity = popcount), seg i64 [F+1],
  *     k = 4 pi dt / lambda, ridge >= 0, bounds4 (host) = {vx_lo, vx_hi, vy_lo, vy_hi};
  *     out f64 [F, 8] = {vx, vy, cost, rmse, max_residual, n, det, 0}; resid/pred f64 [N] nullable. */
-int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask, const void* seg, int F, double k,
-                 double ridge, const double* bounds4, void* out, void* resid, void* pred);
+int rsl_velocity(rsl_handle h, const void* az, const void* gidx, const void* az_table, int G, const void* y,
+                 const void* amask, const void* seg, int F, double k, double ridge, const double* bounds4, void* out,
+                 void* resid, void* pred);
 
 /* a3-a6  SignalPreprocessor.dechirp_signal / apply_window / remove_dc / process_chirp (dechirp.py:85-166):
  *     out[r, s] = in[r, s] * table[s], then (dc != 0) minus the row's complex mean.  in/out c64 [rows, S]. */

@@ -301,13 +301,8 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
     return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
-  int dev = h->device, ncu = 256;
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  long long blocks = (long long)ncu * 4;
-  if (!ncell_dev) {
-    const long long need = (ncell + 127) / 128;  // 4 waves x 32 cells
-    if (need < blocks) blocks = need;
-  }
+  long long blocks = 0;  // 0: all resident workgroups (occupancy x CUs)
+  if (!ncell_dev) blocks = (ncell + 127) / 128;  // 4 waves x 32 cells
   const int ntiles = (2 * G + 15) / 16;
   Scope sc(h, RSL_K_DOA_SCAN);
   return hip_check(h,
@@ -349,17 +344,20 @@ int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const voi
                    "confidence");
 }
 
-int rsl_velocity(rsl_handle h, const void* az, const void* y, const void* amask, const void* seg, int F, double k,
-                 double ridge, const double* bounds4, void* out, void* resid, void* pred) {
+int rsl_velocity(rsl_handle h, const void* az, const void* gidx, const void* az_table, int G, const void* y,
+                 const void* amask, const void* seg, int F, double k, double ridge, const double* bounds4, void* out,
+                 void* resid, void* pred) {
   if (!h) return RSL_ERR_INVALID;
-  if (F < 0 || !az || !y || !seg || !bounds4 || !out) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
+  if (F < 0 || (!az && !gidx) || !y || !seg || !bounds4 || !out)
+    return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
+  if (gidx && (!az_table || G <= 0 || G > 2048)) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad grid table");
   if (!(bounds4[0] <= bounds4[1]) || !(bounds4[2] <= bounds4[3]) || ridge < 0)
     return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad bounds/ridge");
   Scope sc(h, RSL_K_VELOCITY);
   return hip_check(h,
-                   rsl::launch_velocity(h->stream, (const double*)az, (const double*)y, (const unsigned*)amask,
-                                        (const long long*)seg, F, k, ridge, bounds4, (double*)out, (double*)resid,
-                                        (double*)pred),
+                   rsl::launch_velocity(h->stream, (const double*)az, (const int*)gidx, (const double*)az_table, G,
+                                        (const double*)y, (const unsigned*)amask, (const long long*)seg, F, k, ridge,
+                                        bounds4, (double*)out, (double*)resid, (double*)pred),
                    "velocity");
 }
 

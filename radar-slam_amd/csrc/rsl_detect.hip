@@ -149,7 +149,9 @@ __global__ __launch_bounds__(1024) void k_frame_scan(const long long* __restrict
   }
 }
 
-// One thread per (frame, range row, mask word).
+// One wave per (frame, range row): lane j of word w owns Doppler cell 64 w + j.  Ranks inside a word are
+// popcounts of the lower lanes' bits, so every entry/cell index is computed without serial loops and the
+// per-entry stores and RDS reads (power_db) are coalesced across the wave.
 __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, const unsigned long long* __restrict__ mask,
                                               int F, int A, int S, int C, int W,
                                               const int* __restrict__ entry_row_off, const int* __restrict__ cell_row_off,
@@ -159,65 +161,51 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
                                               int* __restrict__ e_dbin, int* __restrict__ e_cell,
                                               double* __restrict__ e_pdb, int* __restrict__ c_frame,
                                               int* __restrict__ c_rc, unsigned* __restrict__ c_amask) {
-  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= (long)F * S * W) return;
-  const int w = gid % W;
-  const int i = (gid / W) % S;
-  const long f = gid / ((long)W * S);
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // f * S + i
+  if (row >= (long)F * S) return;
+  const int lane = threadIdx.x & 63;
+  const long f = row / S;
+  const int i = (int)(row - f * S);
+  const unsigned long long lt = (1ull << lane) - 1ull;
   const unsigned long long* mf = mask + (size_t)f * A * S * W;
-  unsigned long long u = 0;
-  int cpre = 0;
-  for (int ww = 0; ww <= w; ++ww) {
-    unsigned long long uu = 0;
-    for (int a = 0; a < A; ++a) uu |= mf[((size_t)a * S + i) * W + ww];
-    if (ww < w) cpre += __popcll(uu);
-    else u = uu;
-  }
-  if (u == 0) return;
-  const long long cb = cell_base[f] + cell_row_off[f * S + i] + cpre;
-  // cells
-  {
-    unsigned long long m = u;
-    long long c = cb;
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      if (c < cell_cap) {
-        const int j = w * 64 + bit;
-        unsigned am = 0;
-        for (int a = 0; a < A; ++a) am |= (unsigned)((mf[((size_t)a * S + i) * W + w] >> bit) & 1ull) << a;
-        c_frame[c] = (int)f;
-        c_rc[c] = i * C + j;
-        c_amask[c] = am;
-      }
-      ++c;
-    }
-  }
-  // entries, antenna by antenna
   const float2* rf = rds + (size_t)f * A * S * C;
-  for (int a = 0; a < A; ++a) {
-    const unsigned long long* row = mf + ((size_t)a * S + i) * W;
-    unsigned long long m = row[w];
-    if (!m) continue;
-    int epre = 0;
-    for (int ww = 0; ww < w; ++ww) epre += __popcll(row[ww]);
-    long long e = entry_base[f] + entry_row_off[f * A * S + (long)a * S + i] + epre;
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      if (e < entry_cap) {
-        const int j = w * 64 + bit;
-        e_ant[e] = a;
-        e_rbin[e] = i;
-        e_dbin[e] = j;
-        e_cell[e] = (int)(cb + __popcll(u & ((1ull << bit) - 1ull)));
-        if (e_pdb) {
-          const float p = cabs2(rf[((size_t)a * S + i) * C + j]);
-          e_pdb[e] = 10.0 * log10((double)p + 1e-12);
+  long long cnext = cell_base[f] + cell_row_off[row];
+  const long long e0 = entry_base[f];
+  for (int w = 0; w < W; ++w) {
+    unsigned long long u = 0;
+    for (int a = 0; a < A; ++a) u |= mf[((size_t)a * S + i) * W + w];
+    if (u == 0) continue;  // wave-uniform
+    const int j = w * 64 + lane;
+    const bool has = (u >> lane) & 1ull;
+    const long long c = cnext + __popcll(u & lt);
+    unsigned am = 0;
+    for (int a = 0; a < A; ++a) {
+      const unsigned long long m = mf[((size_t)a * S + i) * W + w];
+      if (!m) continue;  // wave-uniform
+      const bool hb = (m >> lane) & 1ull;
+      if (hb) {
+        am |= 1u << a;
+        const unsigned long long* mrow = mf + ((size_t)a * S + i) * W;
+        long long e = e0 + entry_row_off[(size_t)f * A * S + (size_t)a * S + i] + __popcll(m & lt);
+        for (int ww = 0; ww < w; ++ww) e += __popcll(mrow[ww]);
+        if (e < entry_cap) {
+          e_ant[e] = a;
+          e_rbin[e] = i;
+          e_dbin[e] = j;
+          e_cell[e] = (int)c;
+          if (e_pdb) {
+            const float p = cabs2(rf[((size_t)a * S + i) * C + j]);
+            e_pdb[e] = 10.0 * log10((double)p + 1e-12);
+          }
         }
       }
-      ++e;
     }
+    if (has && c < cell_cap) {
+      c_frame[c] = (int)f;
+      c_rc[c] = i * C + j;
+      c_amask[c] = am;
+    }
+    cnext += __popcll(u);
   }
 }
 
@@ -251,8 +239,8 @@ hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long lo
                        int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
   if (F <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
-  const long n = (long)F * S * W;
-  hipLaunchKernelGGL(k_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rds, mask, F, A, S, C, W,
+  const long rows = (long)F * S;
+  hipLaunchKernelGGL(k_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, rds, mask, F, A, S, C, W,
                      entry_row_off, cell_row_off, entry_base, cell_base, entry_cap, cell_cap, e_ant, e_rbin, e_dbin,
                      e_cell, e_pdb, c_frame, c_rc, c_amask);
   return hipGetLastError();

@@ -14,18 +14,54 @@
 // of a 16x16 accumulator holds Re/Im of two grid points of one cell and folds |.|^2 + argmax
 // in registers.  The steering operand lives in LDS in per-lane MFMA order (one ds_read_b128 per
 // tile); 32 cells per wave per pass give two independent accumulator chains.
+#include <cstdlib>
+
 #include "rsl_common.h"
 #include "rsl_internal.h"
 
 namespace rsl {
 
-template <int KS>
+// Loads the B operand (unit-normalised [Re; Im] signature column) of one 16-cell tile for this lane:
+// lane (q, jj) holds S'[k = 4 s + q][cell jj], s < KS.  FAST: A == 2*KS, so the two complex loads for
+// antennas q + 4s' (s' < KS/2) give both the real (slot s') and imaginary (slot s' + KS/2) parts.
+template <int KS, bool FAST>
+RSL_DEV void load_sig(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
+                      long long c, bool ok, int A, int q, size_t plane, size_t fstride, float (&b)[KS]) {
+  const float2* base = rds;
+  if (ok) base = rds + (size_t)cfr[c] * fstride + crc[c];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int s = 0; s < KS / 2; ++s) {
+      float2 z = make_float2(0.f, 0.f);
+      if (ok) z = base[(size_t)(4 * s + q) * plane];
+      b[s] = z.x;
+      b[s + KS / 2] = z.y;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + q;
+      float v = 0.f;
+      if (ok && k < 2 * A) {
+        const int m = k < A ? k : k - A;
+        const float2 z = base[(size_t)m * plane];
+        v = k < A ? z.x : z.y;
+      }
+      b[s] = v;
+    }
+  }
+}
+
+// One wave = 32 cells (two 16-column MFMA tiles) per pass over all grid tiles; the next pass's signature
+// loads are issued before the current pass's MFMAs (software prefetch).  Grid = resident workgroups only
+// (occupancy query), grid-striding over 32-cell chunks, so no tail wave of late workgroups.
+template <int KS, bool FAST, bool MUSIC, bool SPEC, bool GMAX>
 __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
-                                                  const float4* __restrict__ steer, int ntiles, int G, int music,
-                                                  int use_lds, int* __restrict__ out_idx,
-                                                  float* __restrict__ out_gmax, float* __restrict__ out_spec) {
+                                                  const float4* __restrict__ steer, int ntiles, int G, int use_lds,
+                                                  int* __restrict__ out_idx, float* __restrict__ out_gmax,
+                                                  float* __restrict__ out_spec) {
   constexpr int KSG = (KS + 3) / 4;
   extern __shared__ float4 sst[];
   const float4* st = steer;
@@ -40,30 +76,30 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
   const float Mf = (float)A;
   const long long nch = (ncell + 31) >> 5;
-  for (long long ch = (long long)blockIdx.x * 4 + wave; ch < nch; ch += (long long)gridDim.x * 4) {
-    float b[2][KS];
-    float pz[2];
-    bool ok[2];
-    long long cidx[2];
+  const long long stride = (long long)gridDim.x * 4;
+  long long ch = (long long)blockIdx.x * 4 + wave;
+  float nb[2][KS];
+  if (ch < nch) {
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
       const long long c = ch * 32 + t2 * 16 + jj;
-      cidx[t2] = c;
-      ok[t2] = c < ncell;
-      const float2* base = rds;
-      if (ok[t2]) base = rds + (size_t)cfr[c] * fstride + crc[c];
+      load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
+    }
+  }
+  for (; ch < nch; ch += stride) {
+    float b[2][KS];
+    float pz[2];
+    long long cidx[2];
+    bool ok[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      cidx[t2] = ch * 32 + t2 * 16 + jj;
+      ok[t2] = cidx[t2] < ncell;
       float acc = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int k = 4 * s + q;
-        float v = 0.f;
-        if (ok[t2] && k < 2 * A) {
-          const int m = k < A ? k : k - A;
-          const float2 z = base[(size_t)m * plane];
-          v = k < A ? z.x : z.y;
-        }
-        b[t2][s] = v;
-        acc = fmaf(v, v, acc);
+        b[t2][s] = nb[t2][s];
+        acc = fmaf(b[t2][s], b[t2][s], acc);
       }
       acc += __shfl_xor(acc, 16);
       acc += __shfl_xor(acc, 32);
@@ -71,6 +107,15 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
       const float sc = acc > 0.f ? 1.0f / sqrtf(acc) : 1.0f;  // angle_estimation.py:86-88
 #pragma unroll
       for (int s = 0; s < KS; ++s) b[t2][s] *= sc;
+    }
+    // prefetch the next chunk's signatures while this chunk's scan runs
+    const long long nx = ch + stride;
+    if (nx < nch) {
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const long long c = nx * 32 + t2 * 16 + jj;
+        load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
+      }
     }
     float best[2] = {-INFINITY, -INFINITY};
     float bestg[2] = {0.f, 0.f};
@@ -100,20 +145,22 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
           const int g = g0 + h;
           const float re = acc[2 * h], im = acc[2 * h + 1];
           const float gv = fmaf(re, re, im * im);
-          const float den = Mf - gv;
-          const float key = music ? ((den > 1e-12f) ? gv : -1.f) : gv;
-          if (g < G && key > best[t2]) {
+          float key = gv;
+          if constexpr (MUSIC) key = (Mf - gv > 1e-12f) ? gv : -1.f;  // den <= 1e-12 -> spectrum 0
+          if (key > best[t2] && g < G) {
             best[t2] = key;
-            bestg[t2] = gv;
             bidx[t2] = g;
+            if constexpr (GMAX) bestg[t2] = gv;
           }
-          if (out_spec && ok[t2] && g < G) {
-            float val = gv;
-            if (music) {
-              const float d = (pz[t2] > 0.f) ? den : (Mf - 1.f);
-              val = (d > 1e-12f) ? 1.0f / d : 0.f;  // angle_estimation.py:149-152
+          if constexpr (SPEC) {
+            if (ok[t2] && g < G) {
+              float val = gv;
+              if constexpr (MUSIC) {
+                const float d = (pz[t2] > 0.f) ? Mf - gv : (Mf - 1.f);
+                val = (d > 1e-12f) ? 1.0f / d : 0.f;  // angle_estimation.py:149-152
+              }
+              out_spec[(size_t)cidx[t2] * G + g] = val;
             }
-            out_spec[(size_t)cidx[t2] * G + g] = val;
           }
         }
       }
@@ -123,20 +170,233 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
 #pragma unroll
       for (int off = 16; off <= 32; off <<= 1) {
         const float ob = __shfl_xor(best[t2], off);
-        const float og = __shfl_xor(bestg[t2], off);
         const int oi = __shfl_xor(bidx[t2], off);
+        float og = 0.f;
+        if constexpr (GMAX) og = __shfl_xor(bestg[t2], off);
         if (ob > best[t2] || (ob == best[t2] && oi < bidx[t2])) {  // first index wins (np.argmax)
           best[t2] = ob;
-          bestg[t2] = og;
           bidx[t2] = oi;
+          if constexpr (GMAX) bestg[t2] = og;
         }
       }
       if (q == 0 && ok[t2]) {
         out_idx[cidx[t2]] = bidx[t2];
-        if (out_gmax) out_gmax[cidx[t2]] = bestg[t2];
+        if constexpr (GMAX) out_gmax[cidx[t2]] = bestg[t2];
       }
     }
   }
+}
+
+// Argmax-only fast path (no spectrum output).  Per tile and cell column the epilogue is
+//   g0 = re0^2 + im0^2, g1 = re1^2 + im1^2, c = g1 > g0, m = c ? g1 : g0, i = c ? 2t+1 : 2t,
+//   u = m > best, best = u ? m : best, idx = u ? i : idx
+// (10 VALU per 4 MFMA outputs; strict compares keep the first index, as np.argmax).  MUSIC's rule
+// "den = M - g <= 1e-12 -> spectrum 0" can only matter when max g >= M in fp32 (a perfect steering
+// match); such chunks are detected after the scan and re-run with the exact MUSIC key (slow path).
+// NCT = 16-cell column tiles per wave (independent MFMA accumulator chains).
+template <int KS, bool FAST, int NCT, bool KEYED>
+RSL_DEV void argmax_scan(const float4* __restrict__ st, int ntiles, int G, float Mf, int q,
+                         const float (&b)[NCT][KS], float (&best)[NCT], int (&bidx)[NCT]) {
+  constexpr int KSG = (KS + 3) / 4;
+#pragma unroll
+  for (int t2 = 0; t2 < NCT; ++t2) {
+    best[t2] = -INFINITY;
+    bidx[t2] = 0;
+  }
+#pragma unroll 2
+  for (int t = 0; t < ntiles; ++t) {
+    float a[KSG * 4];
+#pragma unroll
+    for (int sg = 0; sg < KSG; ++sg) {
+      const float4 v = st[(t * KSG + sg) * 64 + (threadIdx.x & 63)];
+      a[4 * sg + 0] = v.x;
+      a[4 * sg + 1] = v.y;
+      a[4 * sg + 2] = v.z;
+      a[4 * sg + 3] = v.w;
+    }
+    floatx4 acc[NCT];
+#pragma unroll
+    for (int t2 = 0; t2 < NCT; ++t2) acc[t2] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int t2 = 0; t2 < NCT; ++t2) acc[t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[t2][s], acc[t2], 0, 0, 0);
+    const int i0 = 8 * t + 2 * q;
+    const bool last = (t == ntiles - 1);
+#pragma unroll
+    for (int t2 = 0; t2 < NCT; ++t2) {
+      float g0 = fmaf(acc[t2][0], acc[t2][0], acc[t2][1] * acc[t2][1]);
+      float g1 = fmaf(acc[t2][2], acc[t2][2], acc[t2][3] * acc[t2][3]);
+      if constexpr (KEYED) {  // exact MUSIC key: points with M - g <= 1e-12 never win
+        g0 = (Mf - g0 > 1e-12f) ? g0 : -1.f;
+        g1 = (Mf - g1 > 1e-12f) ? g1 : -1.f;
+      }
+      if (last) {  // zero-padded rows of the last tile never win
+        if (i0 >= G) g0 = -INFINITY;
+        if (i0 + 1 >= G) g1 = -INFINITY;
+      }
+      const bool c = g1 > g0;
+      const float m = c ? g1 : g0;
+      const int ii = c ? i0 + 1 : i0;
+      const bool u = m > best[t2];
+      best[t2] = u ? m : best[t2];
+      bidx[t2] = u ? ii : bidx[t2];
+    }
+  }
+}
+
+template <int KS, bool FAST, int NCT, bool MUSIC, bool GMAX>
+__global__ __launch_bounds__(256) void k_doa_argmax(const float2* __restrict__ rds, int A, int S, int C,
+                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                    const long long* __restrict__ ncell_dev, long long ncell_host,
+                                                    const float4* __restrict__ steer, int ntiles, int G, int use_lds,
+                                                    int* __restrict__ out_idx, float* __restrict__ out_gmax) {
+  constexpr int KSG = (KS + 3) / 4;
+  constexpr int CPW = 16 * NCT;  // cells per wave per pass
+  extern __shared__ float4 sst[];
+  const float4* st = steer;
+  if (use_lds) {
+    for (int x = threadIdx.x; x < ntiles * KSG * 64; x += 256) sst[x] = steer[x];
+    __syncthreads();
+    st = sst;
+  }
+  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, jj = lane & 15;
+  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
+  const float Mf = (float)A;
+  const long long nch = (ncell + CPW - 1) / CPW;
+  const long long stride = (long long)gridDim.x * 4;
+  long long ch = (long long)blockIdx.x * 4 + wave;
+  float nb[NCT][KS];
+  if (ch < nch) {
+#pragma unroll
+    for (int t2 = 0; t2 < NCT; ++t2) {
+      const long long c = ch * CPW + t2 * 16 + jj;
+      load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
+    }
+  }
+  for (; ch < nch; ch += stride) {
+    float b[NCT][KS];
+#pragma unroll
+    for (int t2 = 0; t2 < NCT; ++t2) {
+      float acc = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        b[t2][s] = nb[t2][s];
+        acc = fmaf(b[t2][s], b[t2][s], acc);
+      }
+      acc += __shfl_xor(acc, 16);
+      acc += __shfl_xor(acc, 32);
+      const float sc = acc > 0.f ? 1.0f / sqrtf(acc) : 1.0f;  // angle_estimation.py:86-88
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[t2][s] *= sc;
+    }
+    const long long nx = ch + stride;
+    if (nx < nch) {
+#pragma unroll
+      for (int t2 = 0; t2 < NCT; ++t2) {
+        const long long c = nx * CPW + t2 * 16 + jj;
+        load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
+      }
+    }
+    float best[NCT];
+    int bidx[NCT];
+    argmax_scan<KS, FAST, NCT, false>(st, ntiles, G, Mf, q, b, best, bidx);
+    if constexpr (MUSIC) {
+      bool hit = false;
+#pragma unroll
+      for (int t2 = 0; t2 < NCT; ++t2) hit |= !(Mf - best[t2] > 1e-12f);
+      if (__ballot(hit)) argmax_scan<KS, FAST, NCT, true>(st, ntiles, G, Mf, q, b, best, bidx);  // rare
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < NCT; ++t2) {
+#pragma unroll
+      for (int off = 16; off <= 32; off <<= 1) {
+        const float ob = __shfl_xor(best[t2], off);
+        const int oi = __shfl_xor(bidx[t2], off);
+        const bool take = (ob > best[t2]) | ((ob == best[t2]) & (oi < bidx[t2]));  // first index wins
+        best[t2] = take ? ob : best[t2];
+        bidx[t2] = take ? oi : bidx[t2];
+      }
+      const long long c = ch * CPW + t2 * 16 + jj;
+      if (q == 0 && c < ncell) {
+        out_idx[c] = bidx[t2];
+        if constexpr (GMAX) out_gmax[c] = best[t2];
+      }
+    }
+  }
+}
+
+template <int KS, bool FAST, bool MUSIC, bool GMAX>
+static hipError_t launch_argmax_t(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                                  const int* c_rc, const long long* ncell_dev, long long ncell_host, const float4* stp,
+                                  int ntiles, int G, int use_lds, size_t lds, int* out_idx, float* out_gmax,
+                                  int max_blocks) {
+  constexpr int NCT = 4;
+  auto kern = k_doa_argmax<KS, FAST, NCT, MUSIC, GMAX>;
+  static int per_cu[2] = {-1, -1};
+  int& occ = per_cu[use_lds ? 1 : 0];
+  if (occ < 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+    occ = nb;
+  }
+  int dev = 0, ncu = 256;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  long long blocks = (long long)occ * ncu;
+  if (max_blocks > 0) {
+    const long long need = (max_blocks * 128LL + 16 * NCT * 4 - 1) / (16 * NCT * 4);  // max_blocks was for 128 cells
+    if (blocks > need) blocks = need;
+  }
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
+                     ncell_host, stp, ntiles, G, use_lds, out_idx, out_gmax);
+  return hipGetLastError();
+}
+
+template <int KS, bool FAST, bool MUSIC, bool SPEC, bool GMAX>
+static hipError_t launch_scan_t(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                                const int* c_rc, const long long* ncell_dev, long long ncell_host, const float4* stp,
+                                int ntiles, int G, int use_lds, size_t lds, int* out_idx, float* out_gmax,
+                                float* out_spec, int max_blocks) {
+  auto kern = k_doa_scan<KS, FAST, MUSIC, SPEC, GMAX>;
+  static int per_cu[2] = {-1, -1};  // occupancy per CU for the LDS / no-LDS variants
+  int& occ = per_cu[use_lds ? 1 : 0];
+  if (occ < 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+    occ = nb;
+  }
+  int dev = 0, ncu = 256;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  long long blocks = (long long)occ * ncu;
+  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
+                     ncell_host, stp, ntiles, G, use_lds, out_idx, out_gmax, out_spec);
+  return hipGetLastError();
+}
+
+template <int KS, bool FAST>
+static hipError_t launch_scan_f(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                                const int* c_rc, const long long* ncell_dev, long long ncell_host, const float4* stp,
+                                int ntiles, int G, int music, int use_lds, size_t lds, int* out_idx, float* out_gmax,
+                                float* out_spec, int max_blocks) {
+  const bool spec = out_spec != nullptr, gmax = out_gmax != nullptr;
+#define L(M, SP, GM)                                                                                               \
+  return launch_scan_t<KS, FAST, M, SP, GM>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, \
+                                            use_lds, lds, out_idx, out_gmax, out_spec, max_blocks)
+  if (music) {
+    if (spec) { if (gmax) L(true, true, true); else L(true, true, false); }
+    else { if (gmax) L(true, false, true); else L(true, false, false); }
+  } else {
+    if (spec) { if (gmax) L(false, true, true); else L(false, true, false); }
+    else { if (gmax) L(false, false, true); else L(false, false, false); }
+  }
+#undef L
 }
 
 hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
@@ -149,18 +409,48 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
   const int use_lds = tab_bytes <= 60 * 1024;
   const size_t lds = use_lds ? tab_bytes : 0;
   const float4* stp = reinterpret_cast<const float4*>(steer_tab);
+  const bool fast = (A == 2 * KS);
+  if (!out_spec && getenv("RSL_DOA_FULL") == nullptr) {  // argmax-only fast path
+    const bool gm = out_gmax != nullptr;
+#define AM(n, F_)                                                                                                  \
+  return music ? (gm ? launch_argmax_t<n, F_, true, true>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host,  \
+                                                          stp, ntiles, G, use_lds, lds, out_idx, out_gmax,         \
+                                                          grid_blocks)                                             \
+                     : launch_argmax_t<n, F_, true, false>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, \
+                                                           stp, ntiles, G, use_lds, lds, out_idx, out_gmax,        \
+                                                           grid_blocks))                                           \
+               : (gm ? launch_argmax_t<n, F_, false, true>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, \
+                                                           stp, ntiles, G, use_lds, lds, out_idx, out_gmax,        \
+                                                           grid_blocks)                                            \
+                     : launch_argmax_t<n, F_, false, false>(st, rds, A, S, C, c_frame, c_rc, ncell_dev,            \
+                                                            ncell_host, stp, ntiles, G, use_lds, lds, out_idx,     \
+                                                            out_gmax, grid_blocks))
+    switch (KS) {
+      case 2: if (fast) AM(2, true); AM(2, false);
+      case 4: if (fast) AM(4, true); AM(4, false);
+      case 6: if (fast) AM(6, true); AM(6, false);
+      case 8: if (fast) AM(8, true); AM(8, false);
+      case 1: AM(1, false);
+      case 3: AM(3, false);
+      case 5: AM(5, false);
+      case 7: AM(7, false);
+      default: return hipErrorInvalidValue;
+    }
+#undef AM
+  }
+#define CASE(n)                                                                                                    \
+  case n:                                                                                                          \
+    if (fast && (n % 2 == 0))                                                                                      \
+      return launch_scan_f<n, (n % 2 == 0)>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, \
+                                            music, use_lds, lds, out_idx, out_gmax, out_spec, grid_blocks);        \
+    return launch_scan_f<n, false>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, music,   \
+                                   use_lds, lds, out_idx, out_gmax, out_spec, grid_blocks);
   switch (KS) {
-#define CASE(n)                                                                                                   \
-  case n:                                                                                                         \
-    hipLaunchKernelGGL(k_doa_scan<n>, dim3(grid_blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc,      \
-                       ncell_dev, ncell_host, stp, ntiles, G, music, use_lds, out_idx, out_gmax, out_spec);      \
-    break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
-#undef CASE
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+#undef CASE
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -173,35 +463,50 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
 // ---------------------------------------------------------------------------------------------
 constexpr int kMaxA = 32;
 
-__global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ rds, int A, int S, int C,
+// NA > 0: antenna count fixed at compile time (registers only); NA == 0: runtime A (<= kMaxA).
+template <int NA>
+__global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ rds, int A_rt, int S, int C,
                                                      const int* __restrict__ cfr, const int* __restrict__ crc,
                                                      const long long* __restrict__ ncell_dev, long long ncell_host,
                                                      double esprit_scale, const int* __restrict__ gidx,
                                                      const double* __restrict__ az_table, float2* __restrict__ sig_out,
                                                      double* __restrict__ esprit_deg, double* __restrict__ phase,
                                                      double* __restrict__ az_out) {
+  constexpr int MA = NA > 0 ? NA : kMaxA;
+  const int A = NA > 0 ? NA : A_rt;
   const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
   const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
   if (c >= ncell) return;
   const size_t plane = (size_t)S * C;
   const float2* base = rds + (size_t)cfr[c] * A * plane + crc[c];
-  double sr[kMaxA], si[kMaxA];
+  float2 zf[MA];
+#pragma unroll
+  for (int m = 0; m < MA; ++m)
+    if (m < A) zf[m] = base[(size_t)m * plane];
+  double sr[MA], si[MA];
   double pw = 0.0;
-  for (int m = 0; m < A; ++m) {
-    const float2 z = base[(size_t)m * plane];
-    sr[m] = z.x;
-    si[m] = z.y;
-    pw += sr[m] * sr[m] + si[m] * si[m];
+#pragma unroll
+  for (int m = 0; m < MA; ++m) {
+    if (m < A) {
+      sr[m] = zf[m].x;
+      si[m] = zf[m].y;
+      pw += sr[m] * sr[m] + si[m] * si[m];
+    }
   }
   if (pw > 0.0) {
     const double sc = 1.0 / sqrt(pw);
-    for (int m = 0; m < A; ++m) {
-      sr[m] *= sc;
-      si[m] *= sc;
-    }
+#pragma unroll
+    for (int m = 0; m < MA; ++m)
+      if (m < A) {
+        sr[m] *= sc;
+        si[m] *= sc;
+      }
   }
-  if (sig_out)
-    for (int m = 0; m < A; ++m) sig_out[(size_t)c * A + m] = make_float2((float)sr[m], (float)si[m]);
+  if (sig_out) {
+#pragma unroll
+    for (int m = 0; m < MA; ++m)
+      if (m < A) sig_out[(size_t)c * A + m] = make_float2((float)sr[m], (float)si[m]);
+  }
   if (phase) {
     // s1 * conj(s0)
     const double re = sr[1] * sr[0] + si[1] * si[0];
@@ -211,12 +516,15 @@ __global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ 
   if (az_out && gidx) az_out[c] = az_table[gidx[c]];
   if (esprit_deg) {
     double a = 0, cc = 0, br = 0, bi = 0;
-    for (int m = 0; m + 1 < A; ++m) {
-      a += sr[m] * sr[m] + si[m] * si[m];
-      cc += sr[m + 1] * sr[m + 1] + si[m + 1] * si[m + 1];
-      // conj(x0) * x1
-      br += sr[m] * sr[m + 1] + si[m] * si[m + 1];
-      bi += sr[m] * si[m + 1] - si[m] * sr[m + 1];
+#pragma unroll
+    for (int m = 0; m + 1 < MA; ++m) {
+      if (m + 1 < A) {
+        a += sr[m] * sr[m] + si[m] * si[m];
+        cc += sr[m + 1] * sr[m + 1] + si[m + 1] * si[m + 1];
+        // conj(x0) * x1
+        br += sr[m] * sr[m + 1] + si[m] * si[m + 1];
+        bi += sr[m] * si[m + 1] - si[m] * sr[m + 1];
+      }
     }
     const double hd = 0.5 * (a - cc);
     const double l1 = 0.5 * (a + cc) + sqrt(hd * hd + br * br + bi * bi);
@@ -226,22 +534,25 @@ __global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ 
     } else {        // v = [b, l1 - a]
       v0r = br; v0i = bi; v1r = l1 - a; v1i = 0.0;
     }
-    // u_m = v0 * s_m + v1 * s_{m+1}, m < A-1 ; phi = sum conj(u_m) u_{m+1} / sum |u_m|^2, m < A-2
+    // u_m = v0 s_m + v1 s_{m+1}, m < A-1 ; phi = sum conj(u_m) u_{m+1} / sum |u_m|^2, m < A-2
     double nr = 0, ni = 0, dd = 0;
     double upr = 0, upi = 0;
-    for (int m = 0; m + 1 < A; ++m) {
-      const double ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
-      const double ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
-      if (m > 0) {
-        nr += upr * ur + upi * ui;
-        ni += upr * ui - upi * ur;
-        dd += upr * upr + upi * upi;
+#pragma unroll
+    for (int m = 0; m + 1 < MA; ++m) {
+      if (m + 1 < A) {
+        const double ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
+        const double ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
+        if (m > 0) {
+          nr += upr * ur + upi * ui;
+          ni += upr * ui - upi * ur;
+          dd += upr * upr + upi * upi;
+        }
+        upr = ur;
+        upi = ui;
       }
-      upr = ur;
-      upi = ui;
     }
     double ang = 0.0;
-    if (dd > 0.0) ang = atan2(ni / dd, nr / dd);
+    if (dd > 0.0) ang = atan2(ni, nr);
     esprit_deg[c] = asin(ang * esprit_scale) * (180.0 / 3.14159265358979323846);
   }
 }
@@ -250,11 +561,17 @@ hipError_t launch_cell_extras(hipStream_t st, const float2* rds, int A, int S, i
                               const int* c_rc, const long long* ncell_dev, long long ncell_host, double esprit_scale,
                               const int* gidx, const double* az_table, float2* sig_out, double* esprit_deg,
                               double* phase, double* az_out) {
-  if (A > kMaxA) return hipErrorInvalidValue;
+  if (A > kMaxA || A < 2) return hipErrorInvalidValue;
   if (ncell_host <= 0) return hipSuccess;
   const long long nb = (ncell_host + 255) / 256;
-  hipLaunchKernelGGL(k_cell_extras, dim3((unsigned)nb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
-                     ncell_host, esprit_scale, gidx, az_table, sig_out, esprit_deg, phase, az_out);
+#define GO(NA)                                                                                                   \
+  hipLaunchKernelGGL(k_cell_extras<NA>, dim3((unsigned)nb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,      \
+                     ncell_dev, ncell_host, esprit_scale, gidx, az_table, sig_out, esprit_deg, phase, az_out)
+  if (A == 8) GO(8);
+  else if (A == 16) GO(16);
+  else if (A == 4) GO(4);
+  else GO(0);
+#undef GO
   return hipGetLastError();
 }
 

@@ -42,9 +42,9 @@ hipError_t launch_confidence(hipStream_t st, const float2* rds, int A, int S, in
                              const int* c_rc, long long n, const int* gidx, const double* steer_c128,
                              const double* steer_phase, double* conf_out);
 // K8: batched bounded / ridge least squares velocity solve, one segment per frame.
-hipError_t launch_velocity(hipStream_t st, const double* az, const double* y, const unsigned* amask,
-                           const long long* seg, int F, double k, double ridge, const double* bounds4, double* out,
-                           double* resid, double* pred);
+hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, const double* az_table, int G,
+                           const double* y, const unsigned* amask, const long long* seg, int F, double k, double ridge,
+                           const double* bounds4, double* out, double* resid, double* pred);
 
 }  // namespace rsl
 

@@ -46,8 +46,9 @@ __device__ double qcost(double vx, double vy, double k, double ridge, const doub
          ridge * (vx * vx + vy * vy);
 }
 
-__global__ __launch_bounds__(256) void k_velocity(const double* __restrict__ az, const double* __restrict__ y,
-                                                  const unsigned* __restrict__ amask,
+__global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az, const int* __restrict__ gidx,
+                                                  const double* __restrict__ az_table, int G,
+                                                  const double* __restrict__ y, const unsigned* __restrict__ amask,
                                                   const long long* __restrict__ seg, double k, double ridge,
                                                   double lx, double hx, double ly, double hy,
                                                   double* __restrict__ out, double* __restrict__ resid,
@@ -55,13 +56,25 @@ __global__ __launch_bounds__(256) void k_velocity(const double* __restrict__ az,
   __shared__ double sh[8];
   __shared__ double mom[7];
   __shared__ double sol[2];
+  extern __shared__ double cs_tab[];  // [2G] cos, sin of the grid azimuths (gidx path)
+  const bool tab = gidx != nullptr;
+  if (tab) {
+    for (int g = threadIdx.x; g < G; g += blockDim.x) sincos(az_table[g], &cs_tab[G + g], &cs_tab[g]);
+    __syncthreads();
+  }
   const long f = blockIdx.x;
   const long long b = seg[f], e = seg[f + 1];
   double n = 0, cc = 0, cs = 0, ss = 0, cy = 0, sy = 0, yy = 0;
   for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
     const double w = amask ? (double)__popc(amask[i]) : 1.0;
     double s, c;
-    sincos(az[i], &s, &c);
+    if (tab) {
+      const int g = gidx[i];
+      c = cs_tab[g];
+      s = cs_tab[G + g];
+    } else {
+      sincos(az[i], &s, &c);
+    }
     const double yi = y[i];
     n += w;
     cc += w * c * c;
@@ -122,7 +135,13 @@ __global__ __launch_bounds__(256) void k_velocity(const double* __restrict__ az,
   for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
     const double w = amask ? (double)__popc(amask[i]) : 1.0;
     double s, c;
-    sincos(az[i], &s, &c);
+    if (tab) {
+      const int g = gidx[i];
+      c = cs_tab[g];
+      s = cs_tab[G + g];
+    } else {
+      sincos(az[i], &s, &c);
+    }
     const double pr = k * (vx * c + vy * s);
     const double r = y[i] - pr;
     r2 += w * r * r;
@@ -145,12 +164,13 @@ __global__ __launch_bounds__(256) void k_velocity(const double* __restrict__ az,
   }
 }
 
-hipError_t launch_velocity(hipStream_t st, const double* az, const double* y, const unsigned* amask,
-                           const long long* seg, int F, double k, double ridge, const double* bounds4, double* out,
-                           double* resid, double* pred) {
+hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, const double* az_table, int G,
+                           const double* y, const unsigned* amask, const long long* seg, int F, double k, double ridge,
+                           const double* bounds4, double* out, double* resid, double* pred) {
   if (F <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_velocity, dim3(F), dim3(256), 0, st, az, y, amask, seg, k, ridge, bounds4[0], bounds4[1],
-                     bounds4[2], bounds4[3], out, resid, pred);
+  const size_t lds = gidx ? sizeof(double) * 2 * (size_t)G : 0;
+  hipLaunchKernelGGL(k_velocity, dim3(F), dim3(512), lds, st, az, gidx, az_table, G, y, amask, seg, k, ridge,
+                     bounds4[0], bounds4[1], bounds4[2], bounds4[3], out, resid, pred);
   return hipGetLastError();
 }
 

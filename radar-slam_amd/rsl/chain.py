@@ -106,11 +106,10 @@ class RadarChain:
         ctx.doa(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap, n_dev=self.ncell_dev,
                 out_idx=self.gidx)
         ctx.cell_extras(self.rds, L['c_frame'], L['c_rc'], n=self.cell_cap, n_dev=self.ncell_dev,
-                        esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, gidx=self.gidx,
-                        az_table=self.az_table, bufs=self.ext)
+                        esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, bufs=self.ext)
         if velocity:
-            ctx.velocity(self.ext['az'], self.ext['phase'], self.offs['cell_base'], k=self.k, ridge=cfg.ridge,
-                         bounds=cfg.bounds, amask=L['c_amask'], out=self.vel)
+            ctx.velocity(None, self.ext['phase'], self.offs['cell_base'], k=self.k, ridge=cfg.ridge,
+                         bounds=cfg.bounds, amask=L['c_amask'], out=self.vel, gidx=self.gidx, az_table=self.az_table)
 
     def totals(self):
         eb = self.offs['entry_base'][self.F].item()
@@ -128,5 +127,6 @@ class RadarChain:
                     e_ant=h(L['e_ant'], ne), e_rbin=h(L['e_rbin'], ne), e_dbin=h(L['e_dbin'], ne),
                     e_cell=h(L['e_cell'], ne), e_pdb=h(L['e_pdb'], ne), c_frame=h(L['c_frame'], nc),
                     c_rc=h(L['c_rc'], nc), c_amask=h(L['c_amask'], nc), gidx=h(self.gidx, nc),
-                    esprit=h(self.ext['esprit'], nc), phase=h(self.ext['phase'], nc), az=h(self.ext['az'], nc),
+                    esprit=h(self.ext['esprit'], nc), phase=h(self.ext['phase'], nc),
+                    az=np.radians(self.grid)[h(self.gidx, nc)],
                     velocity=self.vel.cpu().numpy(), grid=self.grid)
