@@ -27,6 +27,10 @@ extern "C" {
 
 #define RSL_METHOD_BEAMFORMING 0
 #define RSL_METHOD_MUSIC 1
+/* rsl_doa method flag: use the Toeplitz f16-MFMA argmax path (requires RSL_STEER_TOEPLITZ from the table build) */
+#define RSL_DOA_TOEPLITZ 0x100
+/* rsl_steer_table_build flags */
+#define RSL_STEER_TOEPLITZ 1
 
 /* kernel ids for rsl_timing_read */
 #define RSL_K_RANGE_FFT 0
@@ -91,21 +95,35 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A,
                   long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin, void* e_dbin, void* e_cell,
                   void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
 
-/* Host helper: MFMA operand layout of a steering table.  steer_c128 is the host [G][M] complex128
+/* Host helper: MFMA operand tables of a steering matrix.  steer_c128 is the host [G][M] complex128
  * matrix of AngleEstimator.generate_steering_vector (angle_estimation.py:92-107) over the azimuth grid
- * (angle_estimation.py:59-60).  rsl_steer_table_floats returns the float count; *ntiles out. */
+ * (angle_estimation.py:59-60).  rsl_steer_table_floats returns the float count of the table; the build
+ * writes (1) the f32 [Re; Im] operand for v_mfma_f32_16x16x4_f32 (*ntiles = its 16-row tiles) and
+ * (2) the Toeplitz-form f16 hi/lo operand for v_mfma_f32_32x32x16_f16, valid when the steering matrix is a
+ * uniform linear array (*flags |= RSL_STEER_TOEPLITZ). */
 long long rsl_steer_table_floats(int G, int M);
-int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_out, int* ntiles);
+int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_out, int* ntiles, int* flags);
 
 /* a11-a16  extract_spatial_signature + music_spectrum / estimate_angle_music / estimate_angle_beamforming
  *     (angle_estimation.py:67-176, 227-251; robust_angle_estimation.py:236-245).
  *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = *ncell_dev if non-null else ncell.
+ *     steer_tab = device copy of the rsl_steer_table_build output; steer_c128 = device fp64 [G][M][2]
+ *     steering matrix (needed by MUSIC with RSL_DOA_TOEPLITZ for its exact fp64 near-degenerate re-scan).
+ *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; ignored when out_spec is requested).
  *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
  *     at the argmax (unit-norm s); out_spec f32 [n, G] (nullable) = MUSIC 1/(M-|a^H s|^2) with the
  *     reference's den > 1e-12 rule, or the beamforming |a^H s|^2. */
 int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
-            const void* ncell_dev, long long ncell, const void* steer_tab, int G, int method, void* out_idx,
-            void* out_gmax, void* out_spec);
+            const void* ncell_dev, long long ncell, const void* steer_tab, const void* steer_c128, int G, int method,
+            void* out_idx, void* out_gmax, void* out_spec);
+
+/* a11-a16 + a15 + a26 fused: the Toeplitz argmax of rsl_doa (requires RSL_STEER_TOEPLITZ) plus, from the same
+ *     signature load, ESPRIT (f64 deg, nullable; angle_estimation.py:178-225, esprit_scale = lambda/(2 pi d))
+ *     and the spatial phase angle(s1 conj(s0)) (f64, nullable; velocity_solver.py:136) of each cell.
+ *     Returns RSL_ERR_UNSUPPORTED when the grid does not fit the Toeplitz path. */
+int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                   const void* ncell_dev, long long ncell, const void* steer_tab, const void* steer_c128, int G,
+                   int method, double esprit_scale, void* out_idx, void* out_gmax, void* esprit_deg, void* phase);
 
 /* a11, a15, a26  normalised signature (c64 [n, A], nullable), ESPRIT closed form (f64 deg, nullable;
  *     angle_estimation.py:178-225 with esprit_scale = lambda / (2 pi d)), spatial phase

@@ -259,14 +259,25 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A,
                    "emit");
 }
 
-long long rsl_steer_table_floats(int G, int M) {
-  if (G <= 0 || M <= 0) return 0;
+static long long steer_f32_floats(int G, int M) {
   const int KS = (2 * M + 3) / 4, KSG = (KS + 3) / 4;
   const long long ntiles = (2LL * G + 15) / 16;
   return ntiles * KSG * 64 * 4;
 }
 
-int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* ntiles_out) {
+static long long steer_toep_floats(int G, int M) {
+  const int KB = M <= 8 ? 1 : 2;
+  long long nt = (G + 31) / 32;
+  nt += nt & 1;
+  return nt * KB * 2 * 64 * 4;
+}
+
+long long rsl_steer_table_floats(int G, int M) {
+  if (G <= 0 || M <= 0) return 0;
+  return steer_f32_floats(G, M) + steer_toep_floats(G, M);
+}
+
+int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* ntiles_out, int* flags_out) {
   if (!steer || !out || G <= 0 || M <= 0 || M > 16) return RSL_ERR_INVALID;
   const int KS = (2 * M + 3) / 4, KSG = (KS + 3) / 4;
   const int ntiles = (2 * G + 15) / 16;
@@ -288,29 +299,74 @@ int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* nt
           out[(((size_t)t * KSG + sg) * 64 + lane) * 4 + e] = (float)v;
         }
   if (ntiles_out) *ntiles_out = ntiles;
+  const int uni = rsl::toep_table_build(steer, G, M, reinterpret_cast<uint16_t*>(out + steer_f32_floats(G, M)),
+                                        nullptr);
+  if (flags_out) *flags_out = (uni && rsl::toep_table_fits(G, M)) ? RSL_STEER_TOEPLITZ : 0;
   return RSL_OK;
 }
 
 int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
-            const void* ncell_dev, long long ncell, const void* steer_tab, int G, int method, void* out_idx,
-            void* out_gmax, void* out_spec) {
+            const void* ncell_dev, long long ncell, const void* steer_tab, const void* steer_c128, int G, int method,
+            void* out_idx, void* out_gmax, void* out_spec) {
   if (!h) return RSL_ERR_INVALID;
   if (A <= 0 || A > 16 || S <= 0 || C <= 0 || G <= 0) return fail(h, RSL_ERR_INVALID, "rsl_doa: bad shape");
   if (!rds || !c_frame || !c_rc || !steer_tab || !out_idx) return fail(h, RSL_ERR_INVALID, "rsl_doa: null pointer");
-  if (method != RSL_METHOD_MUSIC && method != RSL_METHOD_BEAMFORMING)
+  const int base_method = method & 0xff;
+  const bool toep = (method & RSL_DOA_TOEPLITZ) != 0;
+  if (base_method != RSL_METHOD_MUSIC && base_method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
+  const bool music = base_method == RSL_METHOD_MUSIC;
+  if (toep && music && !steer_c128)
+    return fail(h, RSL_ERR_INVALID, "rsl_doa: the Toeplitz MUSIC path needs the fp64 steering table");
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
+  Scope sc(h, RSL_K_DOA_SCAN);
+  if (toep && !out_spec && rsl::toep_table_fits(G, A) && getenv("RSL_DOA_FULL") == nullptr) {
+    int nt32 = (G + 31) / 32;
+    nt32 += nt32 & 1;
+    const float* tp = (const float*)steer_tab + steer_f32_floats(G, A);
+    return hip_check(h,
+                     rsl::launch_doa_toep(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
+                                          (const int*)c_rc, (const long long*)ncell_dev, ncell, tp, nt32, G, music,
+                                          (const double*)steer_c128, (int*)out_idx, (float*)out_gmax, 0.0,
+                                          nullptr, nullptr),
+                     "doa_toep");
+  }
   long long blocks = 0;  // 0: all resident workgroups (occupancy x CUs)
   if (!ncell_dev) blocks = (ncell + 127) / 128;  // 4 waves x 32 cells
   const int ntiles = (2 * G + 15) / 16;
-  Scope sc(h, RSL_K_DOA_SCAN);
   return hip_check(h,
                    rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
                                         (const long long*)ncell_dev, ncell, (const float*)steer_tab, ntiles, G,
-                                        method == RSL_METHOD_MUSIC, (int*)out_idx, (float*)out_gmax,
-                                        (float*)out_spec, (int)blocks),
+                                        music, (int*)out_idx, (float*)out_gmax, (float*)out_spec, (int)blocks),
                    "doa_scan");
+}
+
+int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
+                   const void* ncell_dev, long long ncell, const void* steer_tab, const void* steer_c128, int G,
+                   int method, double esprit_scale, void* out_idx, void* out_gmax, void* esprit_deg, void* phase) {
+  if (!h) return RSL_ERR_INVALID;
+  if (A < 2 || A > 16 || S <= 0 || C <= 0 || G <= 0) return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: bad shape");
+  if (!rds || !c_frame || !c_rc || !steer_tab || !out_idx)
+    return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: null pointer");
+  if (method != RSL_METHOD_MUSIC && method != RSL_METHOD_BEAMFORMING)
+    return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: unknown method");
+  const bool music = method == RSL_METHOD_MUSIC;
+  if (music && !steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: MUSIC needs the fp64 steering table");
+  if (!rsl::toep_table_fits(G, A))
+    return fail(h, RSL_ERR_UNSUPPORTED, "rsl_doa_extras: grid too large for the Toeplitz path (use rsl_doa)");
+  if (!ncell_dev && ncell <= 0) return RSL_OK;
+  hipSetDevice(h->device);
+  Scope sc(h, RSL_K_DOA_SCAN);
+  int nt32 = (G + 31) / 32;
+  nt32 += nt32 & 1;
+  const float* tp = (const float*)steer_tab + steer_f32_floats(G, A);
+  return hip_check(h,
+                   rsl::launch_doa_toep(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
+                                        (const long long*)ncell_dev, ncell, tp, nt32, G, music,
+                                        (const double*)steer_c128, (int*)out_idx, (float*)out_gmax, esprit_scale,
+                                        (double*)esprit_deg, (double*)phase),
+                   "doa_extras");
 }
 
 int rsl_cell_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,

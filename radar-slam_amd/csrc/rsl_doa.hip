@@ -515,44 +515,9 @@ __global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ 
   }
   if (az_out && gidx) az_out[c] = az_table[gidx[c]];
   if (esprit_deg) {
-    double a = 0, cc = 0, br = 0, bi = 0;
-#pragma unroll
-    for (int m = 0; m + 1 < MA; ++m) {
-      if (m + 1 < A) {
-        a += sr[m] * sr[m] + si[m] * si[m];
-        cc += sr[m + 1] * sr[m + 1] + si[m + 1] * si[m + 1];
-        // conj(x0) * x1
-        br += sr[m] * sr[m + 1] + si[m] * si[m + 1];
-        bi += sr[m] * si[m + 1] - si[m] * sr[m + 1];
-      }
-    }
-    const double hd = 0.5 * (a - cc);
-    const double l1 = 0.5 * (a + cc) + sqrt(hd * hd + br * br + bi * bi);
-    double v0r, v0i, v1r, v1i;
-    if (a >= cc) {  // v = [l1 - c, conj(b)]
-      v0r = l1 - cc; v0i = 0.0; v1r = br; v1i = -bi;
-    } else {        // v = [b, l1 - a]
-      v0r = br; v0i = bi; v1r = l1 - a; v1i = 0.0;
-    }
-    // u_m = v0 s_m + v1 s_{m+1}, m < A-1 ; phi = sum conj(u_m) u_{m+1} / sum |u_m|^2, m < A-2
-    double nr = 0, ni = 0, dd = 0;
-    double upr = 0, upi = 0;
-#pragma unroll
-    for (int m = 0; m + 1 < MA; ++m) {
-      if (m + 1 < A) {
-        const double ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
-        const double ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
-        if (m > 0) {
-          nr += upr * ur + upi * ui;
-          ni += upr * ui - upi * ur;
-          dd += upr * upr + upi * upi;
-        }
-        upr = ur;
-        upi = ui;
-      }
-    }
-    double ang = 0.0;
-    if (dd > 0.0) ang = atan2(ni, nr);
+    double nr, ni, dd;
+    esprit_phi<MA>(sr, si, A, nr, ni, dd);
+    const double ang = dd > 0.0 ? atan2(ni, nr) : 0.0;
     esprit_deg[c] = asin(ang * esprit_scale) * (180.0 / 3.14159265358979323846);
   }
 }

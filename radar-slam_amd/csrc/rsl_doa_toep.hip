@@ -1,0 +1,379 @@
+// rsl_doa_toep.hip — K5 fast path: steering-scan argmax (MUSIC / beamforming) through the Toeplitz form of
+// |a^H s|^2 on f16 MFMA with a hi/lo split that keeps fp32-class accuracy.  gfx950 / CDNA4.
+//
+// Replaces (reference src/angle_estimation/angle_estimation.py):
+//   music_spectrum :109-154 + estimate_angle_music :156-176 (argmax only),
+//   estimate_angle_beamforming :227-251; robust_angle_estimation.py estimate_angle_robust :236-245.
+//
+// For a uniform linear array a_m(theta) = a_0 e^{j m phi(theta)} (angle_estimation.py:92-107, positions
+// arange(M) d), so with r_k = sum_n s_{n+k} conj(s_n) (the signature's autocorrelation, k = 0..M-1)
+//     P(theta) = |a^H s|^2 = r_0 + 2 sum_{k>=1} (Re r_k cos k phi + Im r_k sin k phi).
+// That is ONE real dot product of length 2M-1 per (grid point, cell): half the rows of the [Re; Im] GEMM,
+// and no |.|^2 in the epilogue.  The contraction T[G x 2M-1] . R[2M-1 x cells] runs on
+// v_mfma_f32_32x32x16_f16 (16x the f32 MFMA rate).  fp16 alone would leave 2^-11 relative error, so both
+// operands are split, x = x_hi + x_lo (each fp16), and three products are accumulated in fp32:
+//     P ~= T_lo r_hi + T_hi r_lo + T_hi r_hi      (dropped T_lo r_lo ~ 2^-22 |T r|)
+// f16 x f16 products are exact in fp32, so the result is within ~1e-6 |T||r| of the fp32 scan.  The r
+// entries are scaled by 2^8 (exact) so the lo halves stay out of the fp16 subnormal range.
+//
+// MUSIC rule (angle_estimation.py:149-152): the spectrum is 1/(M - P) if M - P > 1e-12 else 0.  That can
+// only change the argmax when max P is within rounding of M (s equal to a steering vector).  Such cells
+// are re-scanned exactly in fp64 from the reference's fp64 steering table (rare, lane-divergent path).
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+namespace rsl {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr float kToepScale = 256.f;
+
+// B operand of one cell for this lane: entries e[16 kb + 8 h + j] of
+// [r0, Re r1, Im r1, ..., Re r_{M-1}, Im r_{M-1}, 0...] (normalised signature, x 2^8), split hi/lo.
+template <int MA, int KB>
+RSL_DEV void toep_operand(const float2 (&s)[MA], int h, half8 (&bhi)[KB], half8 (&blo)[KB]) {
+  float pw = 0.f;
+#pragma unroll
+  for (int m = 0; m < MA; ++m) pw = fmaf(s[m].x, s[m].x, fmaf(s[m].y, s[m].y, pw));
+  const float inv = pw > 0.f ? kToepScale / pw : 0.f;  // angle_estimation.py:86-88 (unit-norm s)
+  float e[16 * KB];
+  e[0] = pw > 0.f ? kToepScale : 0.f;
+#pragma unroll
+  for (int k = 1; k < MA; ++k) {
+    float re = 0.f, im = 0.f;
+#pragma unroll
+    for (int n = 0; n + k < MA; ++n) {  // s_{n+k} conj(s_n)
+      re = fmaf(s[n + k].x, s[n].x, fmaf(s[n + k].y, s[n].y, re));
+      im = fmaf(s[n + k].y, s[n].x, fmaf(-s[n + k].x, s[n].y, im));
+    }
+    e[2 * k - 1] = re * inv;
+    e[2 * k] = im * inv;
+  }
+#pragma unroll
+  for (int x = 2 * MA - 1; x < 16 * KB; ++x) e[x] = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = h ? e[16 * kb + 8 + j] : e[16 * kb + j];
+      const _Float16 hi = (_Float16)v;
+      bhi[kb][j] = hi;
+      blo[kb][j] = (_Float16)(v - (float)hi);
+    }
+  }
+}
+
+template <int MA>
+RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
+                        long long c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
+  // unconditional loads from always-valid addresses (antenna clamped to A-1, cell 0 when out of range),
+  // then a select: no per-antenna branches
+  const long long cc = ok ? c : 0;
+  const float2* base = rds + (size_t)cfr[cc] * fstride + crc[cc];
+#pragma unroll
+  for (int m = 0; m < MA; ++m) {
+    const float2 z = base[(size_t)(m < A ? m : A - 1) * plane];
+    s[m] = (ok && m < A) ? z : make_float2(0.f, 0.f);
+  }
+}
+
+// Max of one 32x32 tile's 16 values held by this lane (v_max3 tree; fmaxf returns one of its inputs exactly).
+RSL_DEV float tile_max(const floatx16& a) {
+  const float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
+  const float m2 = fmaxf(fmaxf(a[6], a[7]), a[8]), m3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
+  const float m4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
+  return fmaxf(fmaxf(fmaxf(m0, m1), m2), fmaxf(fmaxf(m3, m4), a[15]));
+}
+
+// Exact fp64 scan of one cell (MUSIC near-degenerate path): key = P if M - P > 1e-12 else -1, first index.
+template <int MA>
+RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __restrict__ steer64, int& idx,
+                        float& gval) {
+  double sr[MA], si[MA], pw = 0.0;
+#pragma unroll
+  for (int m = 0; m < MA; ++m) {
+    sr[m] = s[m].x;
+    si[m] = s[m].y;
+    pw += sr[m] * sr[m] + si[m] * si[m];
+  }
+  const double sc = pw > 0.0 ? 1.0 / sqrt(pw) : 1.0;
+  double best = -INFINITY, bp = 0.0;
+  int bi = 0;
+  for (int g = 0; g < G; ++g) {
+    const double* a = steer64 + (size_t)g * A * 2;
+    double zr = 0.0, zi = 0.0;
+#pragma unroll
+    for (int m = 0; m < MA; ++m) {
+      if (m < A) {
+        const double ar = a[2 * m], ai = a[2 * m + 1];
+        zr += ar * sr[m] + ai * si[m];
+        zi += ar * si[m] - ai * sr[m];
+      }
+    }
+    const double p = (zr * zr + zi * zi) * sc * sc;
+    const double key = ((double)A - p > 1e-12) ? p : -1.0;
+    if (key > best) {
+      best = key;
+      bi = g;
+      bp = p;
+    }
+  }
+  idx = bi;
+  gval = (float)bp;
+}
+
+// One wave = 32 cells per pass (columns of a 32x32 MFMA tile; lanes l and l+32 share a cell and hold the two
+// K halves).  Grid tiles of 32 grid points are processed in pairs (two independent accumulator chains).
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS>
+__global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
+                                                  const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                  const long long* __restrict__ ncell_dev, long long ncell_host,
+                                                  const uint4* __restrict__ ttab, int ntiles, int G,
+                                                  const double* __restrict__ steer64, int* __restrict__ out_idx,
+                                                  float* __restrict__ out_gmax, double esprit_scale,
+                                                  double* __restrict__ out_esprit, double* __restrict__ out_phase) {
+  extern __shared__ uint4 tt[];  // the whole Toeplitz operand table (<= 64 KiB)
+  const int nvec = ntiles * KB * 2 * 64;
+  for (int x = threadIdx.x; x < nvec; x += 256) tt[x] = ttab[x];
+  __syncthreads();
+  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, n = lane & 31;
+  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
+  const long long nch = (ncell + 31) >> 5;
+  const long long stride = (long long)gridDim.x * 4;
+  long long ch = (long long)blockIdx.x * 4 + wave;
+  const float mthr = ((float)A - 1e-4f) * kToepScale;
+  float2 ns[MA];
+  if (ch < nch) {
+    const long long c = ch * 32 + n;
+    load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
+  }
+  for (; ch < nch; ch += stride) {
+    float2 s[MA];
+#pragma unroll
+    for (int m = 0; m < MA; ++m) s[m] = ns[m];
+    const long long c = ch * 32 + n;
+    const long long nx = ch + stride;
+    if (nx < nch) {  // prefetch the next chunk's signatures while this chunk's scan runs
+      const long long c2 = nx * 32 + n;
+      load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns);
+    }
+    half8 bhi[KB], blo[KB];
+    toep_operand<MA, KB>(s, h, bhi, blo);
+    // Argmax epilogue.  Per tile: the tile max (8 v_max3), a strict '>' record test against the running best,
+    // and a conditional copy of the record tile's 16 values; the in-tile index is resolved once per chunk.
+    // Tiles ascend in g and in-tile values ascend in row ((i&3) + 8(i>>2) + 4h), so the first index wins as
+    // in np.argmax.  Rows past G replicate row G-1 and so never win.
+    float best = -INFINITY;
+    int bt = 0;
+    float sv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sv[i] = 0.f;
+    for (int t = 0; t < ntiles; t += 2) {
+      floatx16 acc0 = {}, acc1 = {};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const uint4 h0 = tt[(((t * KB + kb) * 2) + 0) * 64 + lane];
+        const uint4 l0 = tt[(((t * KB + kb) * 2) + 1) * 64 + lane];
+        const uint4 h1 = tt[((((t + 1) * KB + kb) * 2) + 0) * 64 + lane];
+        const uint4 l1 = tt[((((t + 1) * KB + kb) * 2) + 1) * 64 + lane];
+        const half8 ah0 = __builtin_bit_cast(half8, h0), al0 = __builtin_bit_cast(half8, l0);
+        const half8 ah1 = __builtin_bit_cast(half8, h1), al1 = __builtin_bit_cast(half8, l1);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0, bhi[kb], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1, bhi[kb], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, blo[kb], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, blo[kb], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bhi[kb], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bhi[kb], acc1, 0, 0, 0);
+      }
+      {
+        const float m = tile_max(acc0);
+        const bool u = m > best;
+        best = u ? m : best;
+        bt = u ? t : bt;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = u ? acc0[i] : sv[i];
+      }
+      {
+        const float m = tile_max(acc1);
+        const bool u = m > best;
+        best = u ? m : best;
+        bt = u ? t + 1 : bt;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = u ? acc1[i] : sv[i];
+      }
+    }
+    int ii = 15;
+#pragma unroll
+    for (int i = 14; i >= 0; --i) ii = (sv[i] == best) ? i : ii;
+    int bidx = 32 * bt + 4 * h + (ii & 3) + 8 * (ii >> 2);
+    // merge the two K-half lanes of each cell (first index wins on ties)
+    {
+      const float ob = __shfl_xor(best, 32);
+      const int oi = __shfl_xor(bidx, 32);
+      const bool take = (ob > best) | ((ob == best) & (oi < bidx));
+      best = take ? ob : best;
+      bidx = take ? oi : bidx;
+    }
+    if (bidx >= G) bidx = G - 1;
+    float gval = best * (1.0f / kToepScale);
+    if constexpr (MUSIC) {
+      if (best >= mthr && h == 0 && c < ncell) exact_scan<MA>(s, A, G, steer64, bidx, gval);  // rare
+    }
+    if (h == 0 && c < ncell) {
+      out_idx[c] = bidx;
+      if constexpr (GMAX) out_gmax[c] = gval;
+    }
+    if constexpr (EXTRAS) {
+      // fused K6 (k_cell_extras): lanes h = 0 write ESPRIT (angle_estimation.py:178-225), lanes h = 1 the
+      // spatial phase angle(s1 conj(s0)) (velocity_solver.py:136); both share one fp64 atan2.
+      double sr[MA], si[MA], pw = 0.0;
+#pragma unroll
+      for (int m = 0; m < MA; ++m) {
+        sr[m] = s[m].x;
+        si[m] = s[m].y;
+        pw += sr[m] * sr[m] + si[m] * si[m];
+      }
+      if (pw > 0.0) {
+        const double sc = 1.0 / sqrt(pw);
+#pragma unroll
+        for (int m = 0; m < MA; ++m) {
+          sr[m] *= sc;
+          si[m] *= sc;
+        }
+      }
+      double y, x;
+      bool zero = false;
+      if (h == 0) {
+        double nr, ni, dd;
+        esprit_phi<MA>(sr, si, A, nr, ni, dd);
+        y = ni;
+        x = nr;
+        zero = !(dd > 0.0);
+      } else {
+        y = si[1] * sr[0] - sr[1] * si[0];  // s1 * conj(s0)
+        x = sr[1] * sr[0] + si[1] * si[0];
+      }
+      const double ang = zero ? 0.0 : atan2(y, x);
+      if (c < ncell) {
+        if (h == 0) {
+          if (out_esprit) out_esprit[c] = asin(ang * esprit_scale) * (180.0 / 3.14159265358979323846);
+        } else if (out_phase) {
+          out_phase[c] = ang;
+        }
+      }
+    }
+  }
+}
+
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS>
+static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                                const int* c_rc, const long long* ncell_dev, long long ncell_host, const uint4* tab,
+                                int ntiles, int G, const double* steer64, int* out_idx, float* out_gmax,
+                                double esprit_scale, double* out_esprit, double* out_phase, int max_blocks) {
+  auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS>;
+  const size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;  // caller checks toep_table_fits()
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+  int dev = 0, ncu = 256;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  long long blocks = (long long)nb * ncu;
+  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
+                     ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase);
+  return hipGetLastError();
+}
+
+hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                           const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
+                           int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
+                           double esprit_scale, double* out_esprit, double* out_phase) {
+  if (A < 1 || A > 16 || (ntiles32 & 1)) return hipErrorInvalidValue;
+  if (music && !steer64) return hipErrorInvalidValue;
+  if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
+  const long long max_blocks = ncell_dev ? 0 : (ncell_host + 127) / 128;
+  if (!ncell_dev && ncell_host <= 0) return hipSuccess;
+  const uint4* tab = reinterpret_cast<const uint4*>(toep_tab);
+  const bool gm = out_gmax != nullptr, ex = out_esprit || out_phase;
+#define ARGS                                                                                                     \
+  st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, tab, ntiles32, G, steer64, out_idx, out_gmax,          \
+      esprit_scale, out_esprit, out_phase, (int)max_blocks
+#define GO(MA, KB)                                                                                               \
+  if (music) {                                                                                                   \
+    if (gm) return ex ? launch_toep_t<MA, KB, true, true, true>(ARGS) : launch_toep_t<MA, KB, true, true, false>(ARGS); \
+    return ex ? launch_toep_t<MA, KB, true, false, true>(ARGS) : launch_toep_t<MA, KB, true, false, false>(ARGS);     \
+  }                                                                                                              \
+  if (gm) return ex ? launch_toep_t<MA, KB, false, true, true>(ARGS) : launch_toep_t<MA, KB, false, true, false>(ARGS); \
+  return ex ? launch_toep_t<MA, KB, false, false, true>(ARGS) : launch_toep_t<MA, KB, false, false, false>(ARGS);
+  if (A <= 8) {
+    GO(8, 1)
+  }
+  GO(16, 2)
+#undef GO
+#undef ARGS
+}
+
+bool toep_table_fits(int G, int M) {
+  const int KB = M <= 8 ? 1 : 2;
+  int nt = (G + 31) / 32;
+  nt += nt & 1;
+  return (size_t)nt * KB * 2 * 64 * 16 <= 64 * 1024;
+}
+
+// Host: Toeplitz operand table in MFMA A-operand order.  Returns 0 if the steering matrix is not a uniform
+// linear array (then only the f32 path applies).  Layout: [tile t][k-block kb][part hi/lo][lane][8 halves],
+// lane l = row (l & 31) of the tile, k = 16 kb + 8 (l >> 5) + j.  Tiles are padded to an even count with
+// copies of row G-1.
+int toep_table_build(const double* steer, int G, int M, uint16_t* out, int* ntiles32_out) {
+  const int KB = M <= 8 ? 1 : 2;
+  int nt = (G + 31) / 32;
+  nt += nt & 1;
+  if (ntiles32_out) *ntiles32_out = nt;
+  if (M < 2) return 0;
+  // uniformity: a[g][m] = a[g][0] * (a[g][1] conj(a[g][0]))^m, |a| = 1
+  for (int g = 0; g < G; ++g) {
+    const double* a = steer + (size_t)g * M * 2;
+    const double a0r = a[0], a0i = a[1];
+    if (fabs(a0r * a0r + a0i * a0i - 1.0) > 1e-9) return 0;
+    const double er = a[2] * a0r + a[3] * a0i, ei = a[3] * a0r - a[2] * a0i;  // a1 conj(a0)
+    double pr = a0r, pi = a0i;
+    for (int m = 1; m < M; ++m) {
+      const double nr = pr * er - pi * ei, ni = pr * ei + pi * er;
+      pr = nr;
+      pi = ni;
+      if (fabs(pr - a[2 * m]) > 1e-9 || fabs(pi - a[2 * m + 1]) > 1e-9) return 0;
+    }
+  }
+  for (int t = 0; t < nt; ++t)
+    for (int kb = 0; kb < KB; ++kb)
+      for (int lane = 0; lane < 64; ++lane) {
+        int g = 32 * t + (lane & 31);
+        if (g >= G) g = G - 1;
+        const double* a = steer + (size_t)g * M * 2;
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * kb + 8 * (lane >> 5) + j;
+          double v = 0.0;
+          if (k == 0) {
+            v = 1.0;
+          } else if (k < 2 * M - 1) {
+            const int q = (k + 1) / 2;  // e^{j q phi} = a_q conj(a_0)
+            const double cr = a[2 * q] * a[0] + a[2 * q + 1] * a[1];
+            const double ci = a[2 * q + 1] * a[0] - a[2 * q] * a[1];
+            v = 2.0 * ((k & 1) ? cr : ci);
+          }
+          const _Float16 hi = (_Float16)v;
+          const _Float16 lo = (_Float16)(v - (double)(float)hi);
+          const size_t base = ((((size_t)t * KB + kb) * 2) * 64 + lane) * 8 + j;
+          out[base] = __builtin_bit_cast(uint16_t, hi);
+          out[base + 64 * 8] = __builtin_bit_cast(uint16_t, lo);
+        }
+      }
+  return 1;
+}
+
+}  // namespace rsl

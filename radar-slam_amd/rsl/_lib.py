@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get('RSL_LIBRARY', os.path.join(PKG_ROOT, 'lib', 'librsl.s
 
 RSL_OK, RSL_ERR_INVALID, RSL_ERR_UNSUPPORTED, RSL_ERR_HIP = 0, 1, 2, 3
 METHOD_BEAMFORMING, METHOD_MUSIC = 0, 1
+DOA_TOEPLITZ = 0x100
+STEER_TOEPLITZ = 1
 K_NAMES = ['range_fft', 'doppler_fft', 'detect', 'offsets', 'emit', 'doa_scan', 'cell_extras', 'confidence',
            'velocity', 'aux']
 
@@ -37,8 +39,11 @@ SIGNATURES = {
     'rsl_peak_emit': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_longlong, c_longlong,
                               _P, _P, _P, _P, _P, _P, _P, _P]),
     'rsl_steer_table_floats': (c_longlong, [c_int, c_int]),
-    'rsl_steer_table_build': (c_int, [POINTER(c_double), c_int, c_int, POINTER(c_float), POINTER(c_int)]),
-    'rsl_doa': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, _P, c_int, c_int, _P, _P, _P]),
+    'rsl_steer_table_build': (c_int, [POINTER(c_double), c_int, c_int, POINTER(c_float), POINTER(c_int),
+                                      POINTER(c_int)]),
+    'rsl_doa': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, _P, _P, c_int, c_int, _P, _P, _P]),
+    'rsl_doa_extras': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, _P, _P, c_int, c_int, c_double,
+                               _P, _P, _P, _P]),
     'rsl_cell_extras': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, c_double, _P, _P, _P, _P,
                                 _P, _P]),
     'rsl_confidence': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, c_longlong, _P, _P, _P, _P]),

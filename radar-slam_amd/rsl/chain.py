@@ -94,6 +94,8 @@ class RadarChain:
         self.ext = dict(esprit=e((cc,), torch.float64), phase=e((cc,), torch.float64), az=e((cc,), torch.float64))
         self.vel = e((F, 8), torch.float64)
         self.ncell_dev = self.offs['cell_base'][F:F + 1]
+        # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
+        self.fused_doa = False  # fused DoA + ESPRIT kernel: slower than split so far
 
     def run(self, cube, *, esprit: bool = True, velocity: bool = True):
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""
@@ -103,10 +105,15 @@ class RadarChain:
         ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
         ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists)
         L = self.lists
-        ctx.doa(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap, n_dev=self.ncell_dev,
-                out_idx=self.gidx)
-        ctx.cell_extras(self.rds, L['c_frame'], L['c_rc'], n=self.cell_cap, n_dev=self.ncell_dev,
-                        esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, bufs=self.ext)
+        if self.fused_doa:
+            ctx.doa_extras(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
+                           n_dev=self.ncell_dev, esprit_scale=self.esprit_scale, out_idx=self.gidx,
+                           esprit=self.ext['esprit'] if esprit else None, phase=self.ext['phase'] if velocity else None)
+        else:
+            ctx.doa(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
+                    n_dev=self.ncell_dev, out_idx=self.gidx)
+            ctx.cell_extras(self.rds, L['c_frame'], L['c_rc'], n=self.cell_cap, n_dev=self.ncell_dev,
+                            esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, bufs=self.ext)
         if velocity:
             ctx.velocity(None, self.ext['phase'], self.offs['cell_base'], k=self.k, ridge=cfg.ridge,
                          bounds=cfg.bounds, amask=L['c_amask'], out=self.vel, gidx=self.gidx, az_table=self.az_table)

@@ -173,20 +173,24 @@ class Context:
         n = self.lib.rsl_steer_table_floats(G, M)
         host = np.zeros(n, dtype=np.float32)
         flat = np.ascontiguousarray(steer_c128.astype(np.complex128)).view(np.float64)
-        nt = c_int()
+        nt, fl = c_int(), c_int()
         rc = self.lib.rsl_steer_table_build(flat.ctypes.data_as(ctypes.POINTER(c_double)), G, M,
-                                            host.ctypes.data_as(ctypes.POINTER(c_float)), byref(nt))
+                                            host.ctypes.data_as(ctypes.POINTER(c_float)), byref(nt), byref(fl))
         if rc != 0:
             raise ValueError(f"rsl_steer_table_build failed (G={G}, M={M})")
         torch = self.torch
         ent = dict(G=G, M=M, tab=self.to_dev(host), c128=self.to_dev(flat.copy()),
+                   toeplitz=bool(fl.value & _lib.STEER_TOEPLITZ),
                    phase=self.to_dev(np.angle(steer_c128).astype(np.float64)))
         self._steer_cache[key] = ent
         return ent
 
     # -- a11-a16 ----------------------------------------------------------------------------------
     def doa(self, rds, c_frame, c_rc, steer, method: int, *, n: Optional[int] = None, n_dev=None,
-            want_gmax: bool = False, want_spec: bool = False, out_idx=None):
+            want_gmax: bool = False, want_spec: bool = False, out_idx=None, fast: bool = True):
+        """Steering-scan argmax per cell.  fast=True (default) uses the Toeplitz f16-MFMA path when the
+        steering matrix is a uniform linear array and no spectrum is requested; fast=False forces the f32
+        [Re; Im] MFMA scan."""
         torch = self.torch
         _, A, S, C = rds.shape
         cap = int(c_frame.shape[0]) if n is None else int(n)
@@ -194,10 +198,24 @@ class Context:
         gmax = self.empty((max(cap, 1),), torch.float32) if want_gmax else None
         spec = self.empty((max(cap, 1), steer['G']), torch.float32) if want_spec else None
         self._bind()
+        m = int(method)
+        if fast and steer['toeplitz'] and not want_spec:
+            m |= _lib.DOA_TOEPLITZ
         self.check(self.lib.rsl_doa(self.h, _ptr(rds), A, S, C, _ptr(c_frame), _ptr(c_rc), _ptr(n_dev), cap,
-                                    _ptr(steer['tab']), steer['G'], int(method), _ptr(idx), _ptr(gmax), _ptr(spec)),
-                   'rsl_doa')
+                                    _ptr(steer['tab']), _ptr(steer['c128']), steer['G'], m, _ptr(idx), _ptr(gmax),
+                                    _ptr(spec)), 'rsl_doa')
         return idx, gmax, spec
+
+    def doa_extras(self, rds, c_frame, c_rc, steer, method: int, *, n: int, n_dev=None, esprit_scale: float,
+                   out_idx, esprit=None, phase=None, gmax=None):
+        """Fused Toeplitz DoA argmax + ESPRIT + spatial phase from one signature load (rsl_doa_extras)."""
+        _, A, S, C = rds.shape
+        self._bind()
+        self.check(self.lib.rsl_doa_extras(self.h, _ptr(rds), A, S, C, _ptr(c_frame), _ptr(c_rc), _ptr(n_dev), int(n),
+                                           _ptr(steer['tab']), _ptr(steer['c128']), steer['G'], int(method),
+                                           float(esprit_scale), _ptr(out_idx), _ptr(gmax), _ptr(esprit),
+                                           _ptr(phase)), 'rsl_doa_extras')
+        return out_idx, esprit, phase
 
     def cell_extras(self, rds, c_frame, c_rc, *, n: int, n_dev=None, esprit_scale: float = 1 / math.pi,
                     want_sig=False, want_esprit=False, want_phase=False, gidx=None, az_table=None, bufs=None):

@@ -63,15 +63,17 @@ def test_steer_table_layout():
     st = O.steering_matrix(grid, M)
     n = lib.rsl_steer_table_floats(G, M)
     out = np.zeros(n, np.float32)
-    nt = ctypes.c_int()
+    nt, fl = ctypes.c_int(), ctypes.c_int()
     flat = np.ascontiguousarray(st).view(np.float64)
     rc = lib.rsl_steer_table_build(flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), G, M,
-                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(nt))
-    assert rc == 0 and nt.value == (2 * G + 15) // 16
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(nt),
+                                   ctypes.byref(fl))
+    assert rc == 0 and nt.value == (2 * G + 15) // 16 and fl.value == 1
     rows = np.zeros((nt.value * 16, 2 * M))
     rows[0:2 * G:2] = np.concatenate([st.real, st.imag], axis=1)
     rows[1:2 * G:2] = np.concatenate([-st.imag, st.real], axis=1)
-    tab = out.reshape(nt.value, 1, 64, 4)
+    n32 = nt.value * 64 * 4
+    tab = out[:n32].reshape(nt.value, 1, 64, 4)
     for t in range(nt.value):
         for lane in range(64):
             for s in range(4):
@@ -182,3 +184,64 @@ def test_context_requires_device():
         pytest.skip('device present')
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         rsl.Context(0)
+
+
+def _toeplitz_rows(lib, st):
+    """Decode the Toeplitz f16 hi/lo section of the steering table into T_hi, T_lo [rows, 16*KB]."""
+    G, M = st.shape
+    n = lib.rsl_steer_table_floats(G, M)
+    out = np.zeros(n, np.float32)
+    nt, fl = ctypes.c_int(), ctypes.c_int()
+    flat = np.ascontiguousarray(st).view(np.float64)
+    assert lib.rsl_steer_table_build(flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), G, M,
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(nt),
+                                     ctypes.byref(fl)) == 0
+    KB = 1 if M <= 8 else 2
+    nt32 = (G + 31) // 32
+    nt32 += nt32 & 1
+    h = out[nt.value * 64 * 4 * (1 if M <= 8 else 2):].view(np.float16).reshape(nt32, KB, 2, 64, 8)
+    T = np.zeros((2, nt32 * 32, 16 * KB))
+    for t in range(nt32):
+        for kb in range(KB):
+            for lane in range(64):
+                for j in range(8):
+                    k = 16 * kb + 8 * (lane >> 5) + j
+                    T[0, 32 * t + (lane & 31), k] = h[t, kb, 0, lane, j]
+                    T[1, 32 * t + (lane & 31), k] = h[t, kb, 1, lane, j]
+    return fl.value, T
+
+
+@pytest.mark.parametrize('M', [8, 16, 4])
+def test_toeplitz_table_reproduces_steering_scan(M):
+    """|a^H s|^2 = r0 + 2 sum_k (Re r_k cos k phi + Im r_k sin k phi): the f16 hi/lo Toeplitz operand of the
+    DoA fast path (rsl_doa_toep.hip) reproduces the reference beamforming spectrum to < 1e-6."""
+    import rsl
+    lib = rsl.load()
+    grid = O.azimuth_grid()
+    st = O.steering_matrix(grid, M)
+    flags, T = _toeplitz_rows(lib, st)
+    assert flags == 1
+    G = len(grid)
+    Tf = T[0] + T[1]
+    rs = np.random.RandomState(1)
+    s = rs.randn(20, M) + 1j * rs.randn(20, M)
+    s /= np.linalg.norm(s, axis=1, keepdims=True)
+    e = np.zeros((20, Tf.shape[1]))
+    e[:, 0] = 1.0
+    for k in range(1, M):
+        r = np.sum(s[:, k:] * np.conj(s[:, :M - k]), axis=1)
+        e[:, 2 * k - 1], e[:, 2 * k] = r.real, r.imag
+    P = e @ Tf[:G].T
+    ref = np.abs(s @ st.conj().T) ** 2
+    assert np.abs(P - ref).max() < 1e-6
+    assert (Tf[G:] == Tf[G - 1]).all()  # padding rows replicate the last grid point
+
+
+def test_toeplitz_flag_off_for_nonuniform_array():
+    import rsl
+    lib = rsl.load()
+    grid = O.azimuth_grid()
+    st = O.steering_matrix(grid, 8)
+    st[:, 3] *= np.exp(0.3j)  # not a uniform linear array
+    flags, _ = _toeplitz_rows(lib, st)
+    assert flags == 0
