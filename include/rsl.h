@@ -74,26 +74,29 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
  *     thr_power = 10^(threshold_db/10) - 1e-12 (a cell passes when (double)|rds|^2 > thr_power);
  *     range gate i_lo <= range_bin <= i_hi (from linspace(0, rr*S, S) on the host);
  *     mask u64 [F, A, S, W], W = ceil(C/64) (bit j%64 of word j/64 = peak at doppler j);
- *     row_count i32 [F, A, S];  db_map f32 [F, A, S, C] (nullable) = 10 log10(|rds|^2 + 1e-12). */
+ *     row_count i32 [F, A, S];  db_map f32 [F, A, S, C] (nullable) = 10 log10(|rds|^2 + 1e-12);
+ *     peak_pow f32 [F, A, S, C] (nullable): row-compact |rds|^2 of the peaks, slot = rank within the row. */
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
-               void* mask, void* row_count, void* db_map);
+               void* mask, void* row_count, void* db_map, void* peak_pow);
 
 /* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
  * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
  *     entry_row_off i32 [F*A*S], cell_row_off i32 [F*S], scratch i32 [F*S],
  *     entry_base i64 [F+1], cell_base i64 [F+1] (global exclusive offsets; [F] = totals),
- *     frame_counts i64 [2F] (entries, cells per frame). */
+ *     frame_counts i64 [2F] (entries, cells per frame), union_mask u64 [F, S, W] (nullable) = OR over antennas. */
 int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int F, int A, int S, int C,
                      void* entry_row_off, void* cell_row_off, void* scratch, void* entry_base, void* cell_base,
-                     void* frame_counts);
+                     void* frame_counts, void* union_mask);
 
 /* Emit the peak entries (e_* arrays, i32; e_pdb f64 = per-entry power_db, nullable) and the unique cells
  * (c_frame i32, c_rc i32 = range_bin*C + doppler_bin, c_amask u32 = antennas with a peak there).
- * e_cell maps each entry to its cell.  Items beyond *_cap are dropped (compare the totals). */
-int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A, int S, int C,
-                  const void* entry_row_off, const void* cell_row_off, const void* entry_base, const void* cell_base,
-                  long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin, void* e_dbin, void* e_cell,
-                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
+ * e_cell maps each entry to its cell.  Items beyond *_cap are dropped (compare the totals).
+ * With union_mask (from rsl_peak_offsets) and peak_pow (from rsl_detect) the RDS is not read (rds may be
+ * NULL); otherwise power_db is recomputed from rds. */
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow, int F,
+                  int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
+                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
+                  void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
 
 /* Host helper: MFMA operand tables of a steering matrix.  steer_c128 is the host [G][M] complex128
  * matrix of AngleEstimator.generate_steering_vector (angle_estimation.py:92-107) over the azimuth grid

@@ -205,7 +205,7 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
 }
 
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
-               void* mask, void* row_count, void* db_map) {
+               void* mask, void* row_count, void* db_map, void* peak_pow) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_detect: bad shape");
   if (!rds || !mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_detect: null pointer");
@@ -213,13 +213,13 @@ int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double
   Scope sc(h, RSL_K_DETECT);
   return hip_check(h,
                    rsl::launch_detect(h->stream, (const float2*)rds, F, A, S, C, thr_power, i_lo, i_hi,
-                                      (unsigned long long*)mask, (int*)row_count, (float*)db_map),
+                                      (unsigned long long*)mask, (int*)row_count, (float*)db_map, (float*)peak_pow),
                    "detect");
 }
 
 int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int F, int A, int S, int C,
                      void* entry_row_off, void* cell_row_off, void* scratch, void* entry_base, void* cell_base,
-                     void* frame_counts) {
+                     void* frame_counts, void* union_mask) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || S <= 0 || C <= 0 || A > 32) return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: bad shape");
   if (!mask || !row_count || !entry_row_off || !cell_row_off || !scratch || !entry_base || !cell_base || !frame_counts)
@@ -235,21 +235,33 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
   return hip_check(h,
                    rsl::launch_offsets(h->stream, (const unsigned long long*)mask, (const int*)row_count, F, A, S, C,
                                        (int*)entry_row_off, (int*)cell_row_off, (int*)scratch,
-                                       (long long*)entry_base, (long long*)cell_base, (long long*)frame_counts),
+                                       (long long*)entry_base, (long long*)cell_base, (long long*)frame_counts,
+                                       (unsigned long long*)union_mask),
                    "offsets");
 }
 
-int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, int F, int A, int S, int C,
-                  const void* entry_row_off, const void* cell_row_off, const void* entry_base, const void* cell_base,
-                  long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin, void* e_dbin, void* e_cell,
-                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow, int F,
+                  int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
+                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
+                  void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: bad shape");
-  if (!rds || !mask || !entry_row_off || !cell_row_off || !entry_base || !cell_base)
+  if (!mask || !entry_row_off || !cell_row_off || !entry_base || !cell_base)
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null pointer");
   if ((entry_cap > 0 && (!e_ant || !e_rbin || !e_dbin || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null output");
+  const int W = (C + 63) / 64;
   Scope sc(h, RSL_K_EMIT);
+  if (union_mask && (peak_pow || !e_pdb) && (W & (W - 1)) == 0 && W <= 64)
+    return hip_check(h,
+                     rsl::launch_emit2(h->stream, (const unsigned long long*)mask,
+                                       (const unsigned long long*)union_mask, (const float*)peak_pow, F, A, S, C,
+                                       (const int*)entry_row_off, (const int*)cell_row_off,
+                                       (const long long*)entry_base, (const long long*)cell_base, entry_cap, cell_cap,
+                                       (int*)e_ant, (int*)e_rbin, (int*)e_dbin, (int*)e_cell, (double*)e_pdb,
+                                       (int*)c_frame, (int*)c_rc, (unsigned*)c_amask),
+                     "emit2");
+  if (!rds) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: rds needed without union_mask / peak_pow");
   return hip_check(h,
                    rsl::launch_emit(h->stream, (const float2*)rds, (const unsigned long long*)mask, F, A, S, C,
                                     (const int*)entry_row_off, (const int*)cell_row_off, (const long long*)entry_base,

@@ -18,7 +18,8 @@ constexpr int kDetRows = 16;  // shifted range rows per workgroup
 
 __global__ __launch_bounds__(256) void k_detect(const float2* __restrict__ rds, int S, int C, int W, double thr_p,
                                                 int i_lo, int i_hi, unsigned long long* __restrict__ mask,
-                                                int* __restrict__ row_count, float* __restrict__ dbmap) {
+                                                int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                float* __restrict__ pk_pow) {
   extern __shared__ float pw[];  // (kDetRows + 2) x C power values
   const int nib = (S + kDetRows - 1) / kDetRows;
   const int ib = blockIdx.x % nib;
@@ -55,6 +56,8 @@ __global__ __launch_bounds__(256) void k_detect(const float2* __restrict__ rds, 
       }
       const unsigned long long b = __ballot(pk);
       if (lane == 0) mask[((size_t)fa * S + i) * W + w] = b;
+      if (pk_pow && pk)  // row-compact peak powers: slot = rank of the peak within its row
+        pk_pow[((size_t)fa * S + i) * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = mid[j];
       cnt += __popcll(b);
     }
     if (lane == 0) row_count[(size_t)fa * S + i] = cnt;
@@ -91,7 +94,8 @@ __device__ long long block_scan_global(const int* in, int* out, int n, long long
 __global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __restrict__ mask,
                                                   const int* __restrict__ row_count, int A, int S, int W,
                                                   int* __restrict__ entry_row_off, int* __restrict__ cell_row_off,
-                                                  int* __restrict__ cell_row_cnt, long long* __restrict__ frame_counts) {
+                                                  int* __restrict__ cell_row_cnt, long long* __restrict__ frame_counts,
+                                                  unsigned long long* __restrict__ umask) {
   __shared__ long long lds[1024];
   const long f = blockIdx.x;
   const long long te = block_scan_global(row_count + f * A * S, entry_row_off + f * A * S, A * S, lds);
@@ -102,6 +106,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __re
       unsigned long long u = 0;
       for (int a = 0; a < A; ++a) u |= mf[((size_t)a * S + i) * W + w];
       c += __popcll(u);
+      if (umask) umask[((size_t)f * S + i) * W + w] = u;
     }
     cell_row_cnt[f * S + i] = c;
   }
@@ -209,24 +214,242 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
   }
 }
 
+// Stream compaction of the peak / cell bit masks: 256 consecutive mask words per block produce one contiguous run of
+// entries (or cells).  Phase 1: per-word popcounts, a block scan, and one packed (word, bit) code per item in
+// LDS.  Phase 2: item k of the block is written by lane k % 256, so every store instruction is coalesced
+// (consecutive lanes -> consecutive addresses); scattered 4-byte stores from a per-word set-bit loop would cost
+// one memory request per lane.  Entries follow dechirp.py:257 (np.where order: antenna -> range -> doppler);
+// cells are range-major unions over antennas.  power_db comes from the row-compact peak powers of k_detect
+// (no RDS re-read), 10 log10 in fp32 (the powers are fp32), stored as float64 like power_spectrum_db.  A block with more than kEmitCap items falls back to the per-word loop.
+constexpr int kEmitCap = 4096;
+
+RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int pre = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ws = wsum[k];
+    if (k < wave) pre += ws;
+    total += ws;
+  }
+  return pre + x - v;
+}
+
+template <int W, int MAXA>
+__global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __restrict__ mask,
+                                                    const unsigned long long* __restrict__ umask,
+                                                    const float* __restrict__ pk_pow, long long F, int A, int S,
+                                                    int C, const int* __restrict__ entry_row_off,
+                                                    const int* __restrict__ cell_row_off,
+                                                    const long long* __restrict__ entry_base,
+                                                    const long long* __restrict__ cell_base, long long entry_cap,
+                                                    long long cell_cap, long long nblk_e, int* __restrict__ e_ant,
+                                                    int* __restrict__ e_rbin, int* __restrict__ e_dbin,
+                                                    int* __restrict__ e_cell, double* __restrict__ e_pdb,
+                                                    int* __restrict__ c_frame, int* __restrict__ c_rc,
+                                                    unsigned* __restrict__ c_amask) {
+  __shared__ unsigned pk[kEmitCap];
+  __shared__ int wsum[4];
+  __shared__ int s_loc[256], s_cw[256], s_r0[256];
+  __shared__ unsigned long long s_u[256];
+  __shared__ long long s_first;
+  const int t = threadIdx.x;
+  const bool entries = blockIdx.x < nblk_e;
+  const long long nent = F * A * S * W, ncw = F * S * W;
+  const long long gw = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256 + t;
+  const long long nw = entries ? nent : ncw;
+  unsigned long long m = 0;
+  long long row = 0;
+  int w = 0;
+  if (gw < nw) {
+    m = entries ? mask[gw] : umask[gw];
+    row = gw / W;  // entries: (f*A + a)*S + i ; cells: f*S + i
+    w = (int)(gw - row * W);
+  }
+  const int cnt = __popcll(m);
+  int total;
+  const int loc = block_exclusive_scan(cnt, wsum, total);
+  // the block's first item index: offsets of the first word (earlier words of its row included)
+  if (t == 0) {
+    long long fst;
+    if (entries) {
+      const long long f = row / ((long long)A * S);
+      fst = entry_base[f] + entry_row_off[row];
+      for (int ww = 0; ww < w; ++ww) fst += __popcll(mask[row * W + ww]);
+    } else {
+      const long long f = row / S;
+      fst = cell_base[f] + cell_row_off[row];
+      for (int ww = 0; ww < w; ++ww) fst += __popcll(umask[row * W + ww]);
+    }
+    s_first = fst;
+  }
+  if (total > kEmitCap) {  // rare: dense block, per-word loop with scattered stores
+    __syncthreads();
+    const long long first = s_first;
+    long long k = first + loc;
+    if (entries) {
+      const long long fa = row / S;
+      const int i = (int)(row - fa * S);
+      const long long f = fa / A;
+      int r = 0;
+      long long c = cell_base[f] + cell_row_off[f * S + i];
+      const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
+      for (int ww = 0; ww < w; ++ww) {
+        r += __popcll(mask[row * W + ww]);
+        c += __popcll(urow[ww]);
+      }
+      const unsigned long long u = (m != 0) ? urow[w] : 0ull;
+      while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        if (k < entry_cap) {
+          e_ant[k] = (int)(fa - f * A);
+          e_rbin[k] = i;
+          e_dbin[k] = w * 64 + b;
+          e_cell[k] = (int)(c + __popcll(u & ((1ull << b) - 1ull)));
+          if (e_pdb) e_pdb[k] = (double)(10.0f * log10f(pk_pow[(size_t)row * C + r] + 1e-12f));
+        }
+        ++r;
+        ++k;
+      }
+    } else {
+      const long long f = row / S;
+      const int i = (int)(row - f * S);
+      while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        unsigned am = 0;
+        for (int a = 0; a < A; ++a)
+          am |= (unsigned)((mask[(((size_t)f * A + a) * S + i) * W + w] >> b) & 1ull) << a;
+        if (k < cell_cap) {
+          c_frame[k] = (int)f;
+          c_rc[k] = i * C + w * 64 + b;
+          c_amask[k] = am;
+        }
+        ++k;
+      }
+    }
+    return;
+  }
+  // phase 1: packed (thread, bit) codes + per-word side data
+  {
+    unsigned long long mm = m;
+    int o = loc;
+    while (mm) {
+      const int b = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      pk[o++] = ((unsigned)t << 6) | (unsigned)b;
+    }
+  }
+  s_loc[t] = loc;
+  if (entries && m) {
+    const long long fa = row / S;
+    const int i = (int)(row - fa * S);
+    const long long f = fa / A;
+    int r = 0;
+    int c = (int)(cell_base[f] + cell_row_off[f * S + i]);
+    const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww)
+      if (ww < w) {
+        r += __popcll(mask[row * W + ww]);
+        c += __popcll(urow[ww]);
+      }
+    s_r0[t] = r;
+    s_cw[t] = c;
+    s_u[t] = urow[w];
+  }
+  __syncthreads();
+  const long long first = s_first;
+  // phase 2: coalesced stores, lane k % 256 writes item k
+  for (int k = t; k < total; k += 256) {
+    const unsigned code = pk[k];
+    const int tt = (int)(code >> 6), b = (int)(code & 63);
+    const long long g2 = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256 + tt;
+    const long long rw = g2 / W;
+    const int ww = (int)(g2 - rw * W);
+    const long long e = first + k;
+    if (entries) {
+      if (e < entry_cap) {
+        const long long fa = rw / S;
+        const int i = (int)(rw - fa * S);
+        const long long f = fa / A;
+        const int r = s_r0[tt] + (k - s_loc[tt]);
+        e_ant[e] = (int)(fa - f * A);
+        e_rbin[e] = i;
+        e_dbin[e] = ww * 64 + b;
+        e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
+        if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)rw * C + r] + 1e-12f));  // dechirp.py:235-236
+      }
+    } else if (e < cell_cap) {
+      const long long f = rw / S;
+      const int i = (int)(rw - f * S);
+      unsigned am = 0;
+#pragma unroll
+      for (int a = 0; a < MAXA; ++a)
+        if (a < A) am |= (unsigned)((mask[(((size_t)f * A + a) * S + i) * W + ww] >> b) & 1ull) << a;
+      c_frame[e] = (int)f;
+      c_rc[e] = i * C + ww * 64 + b;
+      c_amask[e] = am;
+    }
+  }
+}
+
+hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
+                        const float* pk_pow, int F, int A, int S, int C, const int* entry_row_off,
+                        const int* cell_row_off, const long long* entry_base, const long long* cell_base,
+                        long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
+                        double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
+  if (F <= 0) return hipSuccess;
+  if (A > 32) return hipErrorInvalidValue;
+  const int W = (C + 63) / 64;
+  const long long nbe = ((long long)F * A * S * W + 255) / 256, nbc = ((long long)F * S * W + 255) / 256;
+  const unsigned nb = (unsigned)(nbe + nbc);
+#define GO(WW)                                                                                                   \
+  hipLaunchKernelGGL((A <= 8 ? k_emit_block<WW, 8> : k_emit_block<WW, 32>), dim3(nb), dim3(256), 0, st, mask,    \
+                     umask, pk_pow, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
+                     entry_cap, cell_cap, nbe, e_ant, e_rbin, e_dbin, e_cell, e_pdb, c_frame, c_rc, c_amask);
+  switch (W) {
+    case 1: GO(1) break;
+    case 2: GO(2) break;
+    case 4: GO(4) break;
+    case 8: GO(8) break;
+    case 16: GO(16) break;
+    case 32: GO(32) break;
+    case 64: GO(64) break;
+    default: return hipErrorInvalidValue;
+  }
+#undef GO
+  return hipGetLastError();
+}
+
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
-                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap) {
+                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow) {
   if (F <= 0 || A <= 0 || S <= 0 || C <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
   const long nblk = (long)F * A * ((S + kDetRows - 1) / kDetRows);
   const size_t lds = sizeof(float) * (kDetRows + 2) * (size_t)C;
   hipLaunchKernelGGL(k_detect, dim3((unsigned)nblk), dim3(256), lds, st, rds, S, C, W, thr_p, i_lo, i_hi, mask,
-                     row_count, dbmap);
+                     row_count, dbmap, pk_pow);
   return hipGetLastError();
 }
 
 hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const int* row_count, int F, int A, int S,
                           int C, int* entry_row_off, int* cell_row_off, int* cell_row_cnt, long long* entry_base,
-                          long long* cell_base, long long* frame_counts) {
+                          long long* cell_base, long long* frame_counts, unsigned long long* umask) {
   if (F <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
   hipLaunchKernelGGL(k_offsets, dim3(F), dim3(1024), 0, st, mask, row_count, A, S, W, entry_row_off, cell_row_off,
-                     cell_row_cnt, frame_counts);
+                     cell_row_cnt, frame_counts, umask);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_frame_scan, dim3(1), dim3(1024), 0, st, frame_counts, F, entry_base, cell_base);

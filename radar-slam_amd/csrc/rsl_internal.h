@@ -16,17 +16,23 @@ hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, 
 
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
-                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap);
+                         int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);
 // Per-frame offsets of peak entries (antenna-major) and union cells (range-major).
 hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const int* row_count, int F, int A, int S,
                           int C, int* entry_row_off, int* cell_row_off, int* cell_row_cnt, long long* entry_base,
-                          long long* cell_base, long long* frame_counts);
+                          long long* cell_base, long long* frame_counts, unsigned long long* umask);
 // Emit compacted entries and cells in reference order.
 hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long long* mask, int F, int A, int S, int C,
                        const int* entry_row_off, const int* cell_row_off, const long long* entry_base,
                        const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
                        int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
 
+// Emit from row-compact peak powers and union masks (no RDS read); W = ceil(C/64) must be a power of two <= 64.
+hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
+                        const float* pk_pow, int F, int A, int S, int C, const int* entry_row_off,
+                        const int* cell_row_off, const long long* entry_base, const long long* cell_base,
+                        long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
+                        double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
 // K5: steering scan on MFMA (f32 16x16x4), argmax; optional spectrum.
 hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,

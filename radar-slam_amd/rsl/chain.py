@@ -83,9 +83,11 @@ class RadarChain:
         self.rds = e((F, A, S, C), torch.complex64)
         self.mask = e((F, A, S, W), torch.int64)
         self.row_count = e((F, A, S), torch.int32)
+        self.peak_pow = e((F, A, S, C), torch.float32)  # row-compact peak powers (detect -> emit)
         self.offs = dict(entry_row_off=e((F * A * S,), torch.int32), cell_row_off=e((F * S,), torch.int32),
                          scratch=e((F * S,), torch.int32), entry_base=e((F + 1,), torch.int64),
-                         cell_base=e((F + 1,), torch.int64), frame_counts=e((2 * F,), torch.int64))
+                         cell_base=e((F + 1,), torch.int64), frame_counts=e((2 * F,), torch.int64),
+                         union_mask=e((F, S, W), torch.int64))
         ec, cc = self.entry_cap, self.cell_cap
         self.lists = dict(e_ant=e((ec,), torch.int32), e_rbin=e((ec,), torch.int32), e_dbin=e((ec,), torch.int32),
                           e_cell=e((ec,), torch.int32), e_pdb=e((ec,), torch.float64),
@@ -101,9 +103,11 @@ class RadarChain:
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""
         ctx, cfg = self.ctx, self.cfg
         ctx.rds(cube, self.table, dc_removal=cfg.dc_removal, out=self.rds, work=self.work)
-        ctx.detect(self.rds, self.thr_p, self.i_lo, self.i_hi, out=dict(mask=self.mask, row_count=self.row_count))
+        ctx.detect(self.rds, self.thr_p, self.i_lo, self.i_hi,
+                   out=dict(mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow))
         ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
-        ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists)
+        ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists,
+                 peak_pow=self.peak_pow)
         L = self.lists
         if self.fused_doa:
             ctx.doa_extras(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,

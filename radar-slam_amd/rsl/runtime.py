@@ -120,9 +120,10 @@ class Context:
         if rc is None:
             rc = self.empty((F, A, S), torch.int32)
         db = self.empty((F, A, S, C), torch.float32) if want_db else None
+        pk = out.get('peak_pow')
         self._bind()
         self.check(self.lib.rsl_detect(self.h, _ptr(rds), F, A, S, C, float(thr_power), int(i_lo), int(i_hi),
-                                       _ptr(mask), _ptr(rc), _ptr(db)), 'rsl_detect')
+                                       _ptr(mask), _ptr(rc), _ptr(db), _ptr(pk)), 'rsl_detect')
         return mask, rc, db
 
     def offsets(self, mask, row_count, C: int, bufs=None):
@@ -135,12 +136,17 @@ class Context:
         eb = b.get('entry_base') if b.get('entry_base') is not None else self.empty((F + 1,), torch.int64)
         cb = b.get('cell_base') if b.get('cell_base') is not None else self.empty((F + 1,), torch.int64)
         fc = b.get('frame_counts') if b.get('frame_counts') is not None else self.empty((2 * F,), torch.int64)
+        um = b.get('union_mask') if b.get('union_mask') is not None else self.empty((F, S, W), torch.int64)
         self._bind()
         self.check(self.lib.rsl_peak_offsets(self.h, _ptr(mask), _ptr(row_count), F, A, S, C, _ptr(eo), _ptr(co),
-                                             _ptr(sc), _ptr(eb), _ptr(cb), _ptr(fc)), 'rsl_peak_offsets')
-        return dict(entry_row_off=eo, cell_row_off=co, scratch=sc, entry_base=eb, cell_base=cb, frame_counts=fc)
+                                             _ptr(sc), _ptr(eb), _ptr(cb), _ptr(fc), _ptr(um)), 'rsl_peak_offsets')
+        return dict(entry_row_off=eo, cell_row_off=co, scratch=sc, entry_base=eb, cell_base=cb, frame_counts=fc,
+                    union_mask=um)
 
-    def emit(self, rds, mask, offs, entry_cap: int, cell_cap: int, want_pdb: bool = True, bufs=None):
+    def emit(self, rds, mask, offs, entry_cap: int, cell_cap: int, want_pdb: bool = True, bufs=None,
+             peak_pow=None):
+        """Compact peak entries and unique cells.  With ``peak_pow`` (from detect) and the offsets' union mask the
+        RDS is not re-read."""
         torch = self.torch
         F, A, S, C = rds.shape
         b = bufs or {}
@@ -154,7 +160,8 @@ class Context:
         c_f, c_rc, c_am = (get('c_frame', cell_cap, torch.int32), get('c_rc', cell_cap, torch.int32),
                            get('c_amask', cell_cap, torch.int32))
         self._bind()
-        self.check(self.lib.rsl_peak_emit(self.h, _ptr(rds), _ptr(mask), F, A, S, C, _ptr(offs['entry_row_off']),
+        self.check(self.lib.rsl_peak_emit(self.h, _ptr(rds), _ptr(mask), _ptr(offs.get('union_mask')),
+                                          _ptr(peak_pow), F, A, S, C, _ptr(offs['entry_row_off']),
                                           _ptr(offs['cell_row_off']), _ptr(offs['entry_base']),
                                           _ptr(offs['cell_base']), int(entry_cap), int(cell_cap), _ptr(e_ant),
                                           _ptr(e_r), _ptr(e_d), _ptr(e_c), _ptr(e_pdb), _ptr(c_f), _ptr(c_rc),
