@@ -79,6 +79,13 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
                void* mask, void* row_count, void* db_map, void* peak_pow);
 
+/* a7 + a8 fused: range FFT, then Doppler FFT + fftshift + RDS store + peak detection in one kernel (the RDS is
+ *     not re-read for detection).  Arguments as rsl_rds and rsl_detect; falls back to the two calls when the
+ *     shape is not covered (C not a power of two <= 1024, or its range-bin tiling does not divide S/2). */
+int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
+                   const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
+                   void* mask, void* row_count, void* db_map, void* peak_pow);
+
 /* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
  * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
  *     entry_row_off i32 [F*A*S], cell_row_off i32 [F*S], scratch i32 [F*S],

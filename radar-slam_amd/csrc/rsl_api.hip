@@ -204,6 +204,40 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
   return hip_check(h, e, "doppler_fft");
 }
 
+int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
+                   const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
+                   void* mask, void* row_count, void* db_map, void* peak_pow) {
+  if (!h) return RSL_ERR_INVALID;
+  if (!mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: null pointer");
+  if (!rsl::doppler_detect_supported(C, S) || A <= 0 || F < 0) {  // unfused: a7 then a8
+    if (int r = rsl_rds(h, cube, F, A, C_total, chirp0, C, S, table, dc_removal, work, rds)) return r;
+    return rsl_detect(h, rds, F, A, S, C, thr_power, i_lo, i_hi, mask, row_count, db_map, peak_pow);
+  }
+  if (chirp0 < 0 || chirp0 + C > C_total) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: bad shape");
+  if (!cube || !table || !work || !rds) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: null pointer");
+  if (!rsl_fft_supported(S)) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_rds_detect: FFT size not supported");
+  if (F == 0) return RSL_OK;
+  hipSetDevice(h->device);
+  float2* tS = twiddles(h, S);
+  float2* tC = twiddles(h, C);
+  if (!tS || !tC) return fail(h, RSL_ERR_HIP, "twiddle table allocation failed");
+  bool sup = true;
+  hipError_t e;
+  {
+    Scope sc(h, RSL_K_RANGE_FFT);
+    e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
+                              dc_removal, (float2*)work, &sup);
+  }
+  if (int r = hip_check(h, e, "range_fft")) return r;
+  {
+    Scope sc(h, RSL_K_DOPPLER_FFT);
+    e = rsl::launch_doppler_detect(h->stream, (const float2*)work, F, A, C, S, tC, (float2*)rds, thr_power, i_lo,
+                                   i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
+                                   (float*)peak_pow, &sup);
+  }
+  return hip_check(h, e, "doppler_detect");
+}
+
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
                void* mask, void* row_count, void* db_map, void* peak_pow) {
   if (!h) return RSL_ERR_INVALID;

@@ -157,8 +157,15 @@ struct Dft {
   }
 };
 
+// LDS position of FFT point x in a padded row: one pad slot after every 8 points.  Radix-8 Stockham writes
+// (stride 8 points = 64 B per lane) and the 8-lane-group pattern of the second stage then land on distinct
+// banks; unpadded they are 4- to 8-way bank conflicts.
+RSL_DEV constexpr int lp(int x) { return x + (x >> 3); }
+// Padded row length for N points.
+constexpr int lp_row(int N) { return N + (N + 7) / 8; }
+
 // One Stockham autosort stage over ROWS independent rows of N points held in LDS
-// (row stride LD complex).  tw[k] = exp(-2 pi i k / N), k < N (fp64-accurate table).
+// (row stride LD complex, padded positions).  tw[k] = exp(-2 pi i k / N), k < N (fp64-accurate table).
 // In place: every thread reads its butterflies' inputs, the block syncs, then writes.
 template <int N, int R, int NS, int ROWS, int NT, int LD>
 RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
@@ -173,7 +180,7 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
       const int row = idx / NB, j = idx - (idx / NB) * NB;
       const float2* src = buf + row * LD;
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[q][r] = src[j + r * NB];
+      for (int r = 0; r < R; ++r) v[q][r] = src[lp(j + r * NB)];
     }
   }
   __syncthreads();
@@ -189,9 +196,10 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
         for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[r * k * STEP]);
       }
       Dft<R>::run(v[q]);
-      float2* dst = buf + row * LD + (j / NS) * NS * R + k;
+      float2* dst = buf + row * LD;
+      const int o = (j / NS) * NS * R + k;
 #pragma unroll
-      for (int r = 0; r < R; ++r) dst[r * NS] = v[q][r];
+      for (int r = 0; r < R; ++r) dst[lp(o + r * NS)] = v[q][r];
     }
   }
   __syncthreads();
@@ -206,10 +214,11 @@ RSL_DEV void fft_run(float2* buf, const float2* tw, int tid) {
   }
 }
 
-// Forward N-point FFT of ROWS rows in LDS.  Caller must __syncthreads() before.
+// Forward N-point FFT of ROWS rows in LDS (padded positions, see lp()).  Caller must __syncthreads() before.
 template <int N, int ROWS, int NT, int LD>
 RSL_DEV void fft_rows(float2* buf, const float2* tw, int tid) {
   static_assert(make_plan(N).n > 0, "unsupported FFT size");
+  static_assert(LD >= lp_row(N), "row stride too small for the padded layout");
   fft_run<N, 0, ROWS, NT, LD>(buf, tw, tid);
 }
 

@@ -13,6 +13,13 @@ namespace rsl {
 
 constexpr int kThreads = 256;
 
+// The largest float t <= thr: for a float p, (double)p > thr  <=>  p > t.
+float threshold_as_float(double thr) {
+  float t = (float)thr;
+  if ((double)t > thr) t = nextafterf(t, -INFINITY);
+  return t;
+}
+
 // Rows per workgroup for an N-point FFT held in LDS (~32 KiB of row data).
 constexpr int rows_for(int N) {
   int r = 4096 / N;
@@ -31,6 +38,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
                                                          const float2* __restrict__ tw, int dc,
                                                          float2* __restrict__ work) {
   constexpr int CB = rows_for(S);
+  constexpr int LD = lp_row(S);
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + S;
@@ -45,38 +53,43 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
   if constexpr (S % 2 == 0) {
     const float4* src4 = reinterpret_cast<const float4*>(src);
     const float4* tab4 = reinterpret_cast<const float4*>(table);
-    float4* buf4 = reinterpret_cast<float4*>(buf);
     for (int idx = tid; idx < CB * S / 2; idx += kThreads) {
       const int r = idx / (S / 2), s2 = idx - r * (S / 2);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float2 lo = make_float2(0.f, 0.f), hi = lo;
       if (r < nrows) {
         const float4 x = src4[(size_t)r * (S / 2) + s2];
         const float4 t = tab4[s2];
-        const float2 lo = cmul(make_float2(x.x, x.y), make_float2(t.x, t.y));
-        const float2 hi = cmul(make_float2(x.z, x.w), make_float2(t.z, t.w));
-        v = make_float4(lo.x, lo.y, hi.x, hi.y);
+        lo = cmul(make_float2(x.x, x.y), make_float2(t.x, t.y));
+        hi = cmul(make_float2(x.z, x.w), make_float2(t.z, t.w));
       }
-      buf4[idx] = v;
+      buf[r * LD + lp(2 * s2)] = lo;
+      buf[r * LD + lp(2 * s2 + 1)] = hi;
     }
   } else {
     for (int idx = tid; idx < CB * S; idx += kThreads) {
       const int r = idx / S, s = idx - r * S;
-      buf[idx] = (r < nrows) ? cmul(src[(size_t)r * S + s], table[s]) : make_float2(0.f, 0.f);
+      buf[r * LD + lp(s)] = (r < nrows) ? cmul(src[(size_t)r * S + s], table[s]) : make_float2(0.f, 0.f);
     }
   }
   __syncthreads();
-  fft_rows<S, CB, kThreads, S>(buf, tws, tid);
+  fft_rows<S, CB, kThreads, LD>(buf, tws, tid);
   if (dc) {
-    if (tid < CB) buf[tid * S] = make_float2(0.f, 0.f);
+    if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
     __syncthreads();
   }
   float2* dst = work + ((size_t)fa * C + cbeg) * S;
   if constexpr (S % 2 == 0) {
     float4* dst4 = reinterpret_cast<float4*>(dst);
-    const float4* buf4 = reinterpret_cast<const float4*>(buf);
-    for (int idx = tid; idx < nrows * S / 2; idx += kThreads) dst4[idx] = buf4[idx];
+    for (int idx = tid; idx < nrows * S / 2; idx += kThreads) {
+      const int r = idx / (S / 2), s2 = idx - r * (S / 2);
+      const float2 lo = buf[r * LD + lp(2 * s2)], hi = buf[r * LD + lp(2 * s2 + 1)];
+      dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    }
   } else {
-    for (int idx = tid; idx < nrows * S; idx += kThreads) dst[idx] = buf[idx];
+    for (int idx = tid; idx < nrows * S; idx += kThreads) {
+      const int r = idx / S, s = idx - r * S;
+      dst[idx] = buf[r * LD + lp(s)];
+    }
   }
 }
 
@@ -90,7 +103,7 @@ template <int C>
 __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restrict__ work, int S,
                                                            const float2* __restrict__ tw, float2* __restrict__ rds) {
   constexpr int KB = rows_for(C);
-  constexpr int LD = (KB == 1) ? C : C + 1;
+  constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + C;
@@ -104,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
   const float2* src = work + (size_t)fa * C * S + k0;
   for (int idx = tid; idx < C * KB; idx += kThreads) {
     const int c = idx / KB, kk = idx - c * KB;
-    buf[kk * LD + c] = (kk < nk) ? src[(size_t)c * S + kk] : make_float2(0.f, 0.f);
+    buf[kk * LD + lp(c)] = (kk < nk) ? src[(size_t)c * S + kk] : make_float2(0.f, 0.f);
   }
   __syncthreads();
   fft_rows<C, KB, kThreads, LD>(buf, tws, tid);
@@ -117,8 +130,121 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
     if (i >= S) i -= S;
     int d = j - hc;  // out[j] = X[(j - C//2) mod C]
     if (d < 0) d += C;
-    dst[(size_t)i * C + j] = buf[kk * LD + d];
+    dst[(size_t)i * C + j] = buf[kk * LD + lp(d)];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2+K3 fused: Doppler FFT, fftshift, RDS store AND peak detection (dechirp.py:208-271) in one pass.
+// The block FFTs KB interior range bins plus one halo bin on each side (KB+2 rows), writes the KB shifted
+// RDS rows, overwrites the LDS tile with |X|^2, and runs the 3x3 'reflect' local-max test, threshold and
+// range gate on the interior rows.  Halo rows are neighbours in shifted range space except across the
+// shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
+// Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
+// ---------------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __restrict__ work, int S,
+                                                             const float2* __restrict__ tw, float2* __restrict__ rds,
+                                                             float thr_f, int i_lo, int i_hi,
+                                                             unsigned long long* __restrict__ mask,
+                                                             int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                             float* __restrict__ pk_pow) {
+  constexpr int KB = rows_for(C);
+  constexpr int NR = KB + 2;
+  constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
+  constexpr int W = (C + 63) / 64;
+  constexpr int PER = (NR * C + kThreads - 1) / kThreads;
+  extern __shared__ float2 sm[];
+  float2* tws = sm;
+  float2* buf = sm + C;
+  const int tid = threadIdx.x;
+  const int nkb = S / KB;
+  const int kb = blockIdx.x % nkb;
+  const long fa = blockIdx.x / nkb;
+  const int k0 = kb * KB;
+  for (int k = tid; k < C; k += kThreads) tws[k] = tw[k];
+  const float2* src = work + (size_t)fa * C * S;
+  for (int idx = tid; idx < C * NR; idx += kThreads) {
+    const int c = idx / NR, r = idx - c * NR;
+    int k = k0 - 1 + r;  // unshifted range bin of LDS row r
+    if (k < 0) k += S;
+    if (k >= S) k -= S;
+    buf[r * LD + lp(c)] = src[(size_t)c * S + k];
+  }
+  __syncthreads();
+  fft_rows<C, NR, kThreads, LD>(buf, tws, tid);
+  const int hs = S / 2, hc = C / 2;
+  int i0 = k0 + hs;  // shifted row of LDS row 1
+  if (i0 >= S) i0 -= S;
+  float2* dst = rds + ((size_t)fa * S + i0) * C;
+  // one pass over the tile: shifted RDS stores (interior rows) and |X|^2 kept in registers
+  float pr[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * kThreads;
+    pr[q] = 0.f;
+    if (idx < NR * C) {
+      const int r = idx / C, j = idx - r * C;  // j: shifted doppler index
+      int d = j - hc;                          // out[j] = X[(j - C//2) mod C]
+      if (d < 0) d += C;
+      const float2 z = buf[r * LD + lp(d)];
+      if (r >= 1 && r <= KB) dst[(size_t)(r - 1) * C + j] = z;
+      pr[q] = cabs2(z);
+    }
+  }
+  __syncthreads();
+  float* pw = reinterpret_cast<float*>(buf);  // power tile [NR][C], shifted doppler order
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * kThreads;
+    if (idx < NR * C) pw[idx] = pr[q];
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int kk = wave; kk < KB; kk += kThreads / 64) {
+    const int i = i0 + kk;
+    const bool gate = (i >= i_lo && i <= i_hi);
+    const bool has_up = i > 0, has_dn = i + 1 < S;
+    const float* up = pw + kk * C;
+    const float* mid = up + C;
+    const float* dn = mid + C;
+    const size_t row = (size_t)fa * S + i;
+    int cnt = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int j = w * 64 + lane;
+      bool pk = false;
+      float p = 0.f;
+      if (j < C) {
+        // 3x3 window max with 'reflect' edges (an out-of-range neighbour repeats an in-window cell)
+        const int jl = j > 0 ? j - 1 : j, jr = j + 1 < C ? j + 1 : j;
+        p = mid[j];
+        float m = fmaxf(fmaxf(mid[jl], p), mid[jr]);
+        if (has_up) m = fmaxf(m, fmaxf(fmaxf(up[jl], up[j]), up[jr]));
+        if (has_dn) m = fmaxf(m, fmaxf(fmaxf(dn[jl], dn[j]), dn[jr]));
+        pk = gate && (p > thr_f) && (p >= m);
+        if (dbmap) dbmap[row * C + j] = 10.f * log10f(p + 1e-12f);
+      }
+      const unsigned long long b = __ballot(pk);
+      if (lane == 0) mask[row * W + w] = b;
+      if (pk_pow && pk) pk_pow[row * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = p;
+      cnt += __popcll(b);
+    }
+    if (lane == 0) row_count[row] = cnt;
+  }
+}
+
+template <int C>
+static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
+                             double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
+                             float* pk_pow) {
+  constexpr int KB = rows_for(C);
+  const long nblk = (long)F * A * (S / KB);
+  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * (lp_row(C) | 1));
+  const float thr_f = threshold_as_float(thr_p);
+  hipLaunchKernelGGL(k_doppler_detect<C>, dim3((unsigned)nblk), dim3(kThreads), lds, st, work, S, tw, rds, thr_f, i_lo,
+                     i_hi, mask, row_count, dbmap, pk_pow);
+  return hipGetLastError();
 }
 
 template <int S>
@@ -126,7 +252,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
                             const float2* table, const float2* tw, int dc, float2* work) {
   constexpr int CB = rows_for(S);
   const long nblk = (long)F * A * ((C + CB - 1) / CB);
-  const size_t lds = sizeof(float2) * (S + (size_t)CB * S);
+  const size_t lds = sizeof(float2) * (S + (size_t)CB * lp_row(S));
   hipLaunchKernelGGL(k_range_fft<S>, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, table, tw,
                      dc, work);
   return hipGetLastError();
@@ -137,7 +263,7 @@ static hipError_t launch_k2(hipStream_t st, const float2* work, int F, int A, in
                             float2* rds) {
   constexpr int KB = rows_for(C);
   const long nblk = (long)F * A * ((S + KB - 1) / KB);
-  const size_t lds = sizeof(float2) * (C + (size_t)KB * ((KB == 1) ? C : C + 1));
+  const size_t lds = sizeof(float2) * (C + (size_t)KB * (lp_row(C) | 1));
   hipLaunchKernelGGL(k_doppler_fft<C>, dim3((unsigned)nblk), dim3(kThreads), lds, st, work, S, tw, rds);
   return hipGetLastError();
 }
@@ -224,6 +350,29 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
 
 #define RSL_FFT_SIZES(X) \
   X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048) X(4096) X(25) X(50) X(100) X(200) X(400) X(800) X(1600)
+
+bool doppler_detect_supported(int C, int S) {
+  if (!fft_supported(C) || (C & (C - 1)) != 0 || C < 8 || C > 1024 || (S & 1)) return false;  // LDS <= 64 KiB
+  const int KB = rows_for(C);
+  return S % KB == 0 && (S / 2) % KB == 0;
+}
+
+hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
+                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported) {
+  *supported = doppler_detect_supported(C, S);
+  if (!*supported || F <= 0 || A <= 0) return hipSuccess;
+  switch (C) {
+#define CASE(n) \
+  case n:       \
+    return launch_k2d<n>(st, work, F, A, S, tw_C, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+    CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
+#undef CASE
+    default:
+      *supported = false;
+      return hipSuccess;
+  }
+}
 
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
                             const float2* table, const float2* tw_S, int dc, float2* work, bool* supported) {

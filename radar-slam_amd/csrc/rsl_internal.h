@@ -14,6 +14,13 @@ hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, in
 hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                               float2* rds, bool* supported);
 
+// K2+K3 fused (Doppler FFT + fftshift + RDS store + detection); supported when C is a power of two and the
+// block's KB range bins tile both halves of S.
+bool doppler_detect_supported(int C, int S);
+float threshold_as_float(double thr);  // largest float t <= thr
+hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
+                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);

@@ -34,6 +34,8 @@ SIGNATURES = {
     'rsl_timing_reset': (c_int, [_P]),
     'rsl_timing_read': (c_int, [_P, c_int, POINTER(c_double), POINTER(c_longlong)]),
     'rsl_rds': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
+    'rsl_rds_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_double, c_int,
+                               c_int, _P, _P, _P, _P]),
     'rsl_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_int, c_int, _P, _P, _P, _P]),
     'rsl_peak_offsets': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P]),
     'rsl_peak_emit': (c_int, [_P, _P, _P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_longlong,

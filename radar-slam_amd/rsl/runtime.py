@@ -106,6 +106,19 @@ class Context:
                                     _ptr(work), _ptr(out)), 'rsl_rds')
         return out
 
+    # -- a7 + a8 fused -----------------------------------------------------------------------------
+    def rds_detect(self, cube, table, thr_power: float, i_lo: int, i_hi: int, *, rds, work, mask, row_count,
+                   peak_pow=None, db_map=None, chirp0: int = 0, num_chirps: Optional[int] = None,
+                   dc_removal: bool = True):
+        """cube [F, A, Ct, S] -> rds [F, A, S, C] + detection outputs, Doppler FFT and detection in one kernel."""
+        F, A, Ct, S = cube.shape
+        C = Ct - chirp0 if num_chirps is None else num_chirps
+        self._bind()
+        self.check(self.lib.rsl_rds_detect(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table), int(dc_removal),
+                                           _ptr(work), _ptr(rds), float(thr_power), int(i_lo), int(i_hi), _ptr(mask),
+                                           _ptr(row_count), _ptr(db_map), _ptr(peak_pow)), 'rsl_rds_detect')
+        return rds
+
     # -- a8 -------------------------------------------------------------------------------------
     def detect(self, rds, thr_power: float, i_lo: int, i_hi: int, want_db: bool = False, out=None):
         torch = self.torch
