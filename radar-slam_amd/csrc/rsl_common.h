@@ -225,9 +225,9 @@ RSL_DEV void fft_rows(float2* buf, const float2* tw, int tid) {
 // ESPRIT closed form (reference angle_estimation.py:178-225) on a unit-norm fp64 signature s (A antennas):
 // svd of X = [s[:-1], s[1:]] -> U[:,0] = u proportional to X v, v = principal eigenvector of the 2x2 Hermitian
 // X^H X; pinv(U1) U2 = u[:-1]^H u[1:] / u[:-1]^H u[:-1] = (nr + i ni) / dd.  The scale/phase of u cancels.
-template <int MA>
-RSL_DEV void esprit_phi(const double (&sr)[MA], const double (&si)[MA], int A, double& nr, double& ni, double& dd) {
-  double a = 0, cc = 0, br = 0, bi = 0;
+template <int MA, typename T>
+RSL_DEV void esprit_phi(const T (&sr)[MA], const T (&si)[MA], int A, T& nr, T& ni, T& dd) {
+  T a = 0, cc = 0, br = 0, bi = 0;
 #pragma unroll
   for (int m = 0; m + 1 < MA; ++m) {
     if (m + 1 < A) {
@@ -237,9 +237,9 @@ RSL_DEV void esprit_phi(const double (&sr)[MA], const double (&si)[MA], int A, d
       bi += sr[m] * si[m + 1] - si[m] * sr[m + 1];
     }
   }
-  const double hd = 0.5 * (a - cc);
-  const double l1 = 0.5 * (a + cc) + sqrt(hd * hd + br * br + bi * bi);
-  double v0r, v0i, v1r, v1i;
+  const T hd = T(0.5) * (a - cc);
+  const T l1 = T(0.5) * (a + cc) + sqrt(hd * hd + br * br + bi * bi);
+  T v0r, v0i, v1r, v1i;
   if (a >= cc) {  // v = [l1 - c, conj(b)]
     v0r = l1 - cc; v0i = 0.0; v1r = br; v1i = -bi;
   } else {        // v = [b, l1 - a]
@@ -247,12 +247,12 @@ RSL_DEV void esprit_phi(const double (&sr)[MA], const double (&si)[MA], int A, d
   }
   // u_m = v0 s_m + v1 s_{m+1}, m < A-1 ; phi = sum conj(u_m) u_{m+1} / sum |u_m|^2, m < A-2
   nr = 0; ni = 0; dd = 0;
-  double upr = 0, upi = 0;
+  T upr = 0, upi = 0;
 #pragma unroll
   for (int m = 0; m + 1 < MA; ++m) {
     if (m + 1 < A) {
-      const double ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
-      const double ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
+      const T ur = v0r * sr[m] - v0i * si[m] + v1r * sr[m + 1] - v1i * si[m + 1];
+      const T ui = v0r * si[m] + v0i * sr[m] + v1r * si[m + 1] + v1i * sr[m + 1];
       if (m > 0) {
         nr += upr * ur + upi * ui;
         ni += upr * ui - upi * ur;

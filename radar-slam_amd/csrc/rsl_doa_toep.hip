@@ -160,6 +160,46 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
       const long long c2 = nx * 32 + n;
       load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns);
     }
+    if constexpr (EXTRAS) {
+      // fused K6 (k_cell_extras), before the scan so its registers are dead during the MFMA loop: lanes h = 0
+      // write ESPRIT (angle_estimation.py:178-225), lanes h = 1 the spatial phase angle(s1 conj(s0))
+      // (velocity_solver.py:136).  fp32 closed form from the fp32 signature, fp64 asin.
+      float sr[MA], si[MA], pw = 0.f;
+#pragma unroll
+      for (int m = 0; m < MA; ++m) {
+        sr[m] = s[m].x;
+        si[m] = s[m].y;
+        pw = fmaf(sr[m], sr[m], fmaf(si[m], si[m], pw));
+      }
+      if (pw > 0.f) {
+        const float sc = 1.0f / sqrtf(pw);
+#pragma unroll
+        for (int m = 0; m < MA; ++m) {
+          sr[m] *= sc;
+          si[m] *= sc;
+        }
+      }
+      float y, x;
+      bool zero = false;
+      if (h == 0) {
+        float nr, ni, dd;
+        esprit_phi<MA>(sr, si, A, nr, ni, dd);
+        y = ni;
+        x = nr;
+        zero = !(dd > 0.f);
+      } else {
+        y = si[1] * sr[0] - sr[1] * si[0];  // s1 * conj(s0)
+        x = sr[1] * sr[0] + si[1] * si[0];
+      }
+      const float ang = zero ? 0.f : atan2f(y, x);
+      if (c < ncell) {
+        if (h == 0) {
+          if (out_esprit) out_esprit[c] = asin((double)ang * esprit_scale) * (180.0 / 3.14159265358979323846);
+        } else if (out_phase) {
+          out_phase[c] = (double)ang;
+        }
+      }
+    }
     half8 bhi[KB], blo[KB];
     toep_operand<MA, KB>(s, h, bhi, blo);
     // Argmax epilogue.  Per tile: the tile max (8 v_max3), a strict '>' record test against the running best,
@@ -225,45 +265,6 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
     if (h == 0 && c < ncell) {
       out_idx[c] = bidx;
       if constexpr (GMAX) out_gmax[c] = gval;
-    }
-    if constexpr (EXTRAS) {
-      // fused K6 (k_cell_extras): lanes h = 0 write ESPRIT (angle_estimation.py:178-225), lanes h = 1 the
-      // spatial phase angle(s1 conj(s0)) (velocity_solver.py:136); both share one fp64 atan2.
-      double sr[MA], si[MA], pw = 0.0;
-#pragma unroll
-      for (int m = 0; m < MA; ++m) {
-        sr[m] = s[m].x;
-        si[m] = s[m].y;
-        pw += sr[m] * sr[m] + si[m] * si[m];
-      }
-      if (pw > 0.0) {
-        const double sc = 1.0 / sqrt(pw);
-#pragma unroll
-        for (int m = 0; m < MA; ++m) {
-          sr[m] *= sc;
-          si[m] *= sc;
-        }
-      }
-      double y, x;
-      bool zero = false;
-      if (h == 0) {
-        double nr, ni, dd;
-        esprit_phi<MA>(sr, si, A, nr, ni, dd);
-        y = ni;
-        x = nr;
-        zero = !(dd > 0.0);
-      } else {
-        y = si[1] * sr[0] - sr[1] * si[0];  // s1 * conj(s0)
-        x = sr[1] * sr[0] + si[1] * si[0];
-      }
-      const double ang = zero ? 0.0 : atan2(y, x);
-      if (c < ncell) {
-        if (h == 0) {
-          if (out_esprit) out_esprit[c] = asin(ang * esprit_scale) * (180.0 / 3.14159265358979323846);
-        } else if (out_phase) {
-          out_phase[c] = ang;
-        }
-      }
     }
   }
 }

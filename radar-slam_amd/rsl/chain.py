@@ -97,7 +97,7 @@ class RadarChain:
         self.vel = e((F, 8), torch.float64)
         self.ncell_dev = self.offs['cell_base'][F:F + 1]
         # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
-        self.fused_doa = False  # fused DoA + ESPRIT kernel: slower than split so far
+        self.fused_doa = bool(self.steer['toeplitz']) and A >= 2
 
     def run(self, cube, *, esprit: bool = True, velocity: bool = True):
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""
