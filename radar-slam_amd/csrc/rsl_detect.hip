@@ -257,9 +257,10 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
                                                     int* __restrict__ e_cell, double* __restrict__ e_pdb,
                                                     int* __restrict__ c_frame, int* __restrict__ c_rc,
                                                     unsigned* __restrict__ c_amask) {
-  __shared__ unsigned pk[kEmitCap];
+  __shared__ unsigned pk[kEmitCap];   // item code: (word << 6) | bit
+  __shared__ unsigned pam[kEmitCap];  // cells: antenna mask of the item
   __shared__ int wsum[4];
-  __shared__ int s_loc[256], s_cw[256], s_r0[256];
+  __shared__ int s_loc[256], s_cw[256], s_r0[256], s_fi[256];
   __shared__ unsigned long long s_u[256];
   __shared__ long long s_first;
   const int t = threadIdx.x;
@@ -268,13 +269,14 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   const long long gw = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256 + t;
   const long long nw = entries ? nent : ncw;
   unsigned long long m = 0;
-  long long row = 0;
-  int w = 0;
-  if (gw < nw) {
-    m = entries ? mask[gw] : umask[gw];
-    row = gw / W;  // entries: (f*A + a)*S + i ; cells: f*S + i
-    w = (int)(gw - row * W);
-  }
+  if (gw < nw) m = entries ? mask[gw] : umask[gw];
+  // word -> (row, w); entries: row = (f*A + a)*S + i, cells: row = f*S + i  (divisions once per word)
+  const long long row = gw / W;
+  const int w = (int)(gw - row * W);
+  const long long q = row / S;  // entries: f*A + a ; cells: f
+  const int i = (int)(row - q * S);
+  const long long f = entries ? q / A : q;
+  const int a = entries ? (int)(q - f * A) : 0;
   const int cnt = __popcll(m);
   int total;
   const int loc = block_exclusive_scan(cnt, wsum, total);
@@ -282,124 +284,108 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   if (t == 0) {
     long long fst;
     if (entries) {
-      const long long f = row / ((long long)A * S);
       fst = entry_base[f] + entry_row_off[row];
       for (int ww = 0; ww < w; ++ww) fst += __popcll(mask[row * W + ww]);
     } else {
-      const long long f = row / S;
       fst = cell_base[f] + cell_row_off[row];
       for (int ww = 0; ww < w; ++ww) fst += __popcll(umask[row * W + ww]);
     }
     s_first = fst;
   }
+  unsigned long long u = 0;  // entries: the union word of (f, i, w)
+  int r0 = 0, cw = 0;
+  if (entries && m) {
+    const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
+    cw = (int)(cell_base[f] + cell_row_off[f * S + i]);
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww)
+      if (ww < w) {
+        r0 += __popcll(mask[row * W + ww]);
+        cw += __popcll(urow[ww]);
+      }
+    u = urow[w];
+  }
+  unsigned long long ma[MAXA];  // cells: the antennas' peak words of (f, i, w)
+  if (!entries && m) {
+#pragma unroll
+    for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
+  }
   if (total > kEmitCap) {  // rare: dense block, per-word loop with scattered stores
     __syncthreads();
-    const long long first = s_first;
-    long long k = first + loc;
-    if (entries) {
-      const long long fa = row / S;
-      const int i = (int)(row - fa * S);
-      const long long f = fa / A;
-      int r = 0;
-      long long c = cell_base[f] + cell_row_off[f * S + i];
-      const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
-      for (int ww = 0; ww < w; ++ww) {
-        r += __popcll(mask[row * W + ww]);
-        c += __popcll(urow[ww]);
-      }
-      const unsigned long long u = (m != 0) ? urow[w] : 0ull;
-      while (m) {
-        const int b = __ffsll((long long)m) - 1;
-        m &= m - 1;
+    long long k = s_first + loc;
+    int r = r0;
+    while (m) {
+      const int b = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      if (entries) {
         if (k < entry_cap) {
-          e_ant[k] = (int)(fa - f * A);
+          e_ant[k] = a;
           e_rbin[k] = i;
           e_dbin[k] = w * 64 + b;
-          e_cell[k] = (int)(c + __popcll(u & ((1ull << b) - 1ull)));
+          e_cell[k] = cw + __popcll(u & ((1ull << b) - 1ull));
           if (e_pdb) e_pdb[k] = (double)(10.0f * log10f(pk_pow[(size_t)row * C + r] + 1e-12f));
         }
-        ++r;
-        ++k;
-      }
-    } else {
-      const long long f = row / S;
-      const int i = (int)(row - f * S);
-      while (m) {
-        const int b = __ffsll((long long)m) - 1;
-        m &= m - 1;
+      } else if (k < cell_cap) {
         unsigned am = 0;
-        for (int a = 0; a < A; ++a)
-          am |= (unsigned)((mask[(((size_t)f * A + a) * S + i) * W + w] >> b) & 1ull) << a;
-        if (k < cell_cap) {
-          c_frame[k] = (int)f;
-          c_rc[k] = i * C + w * 64 + b;
-          c_amask[k] = am;
-        }
-        ++k;
+#pragma unroll
+        for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
+        c_frame[k] = (int)f;
+        c_rc[k] = i * C + w * 64 + b;
+        c_amask[k] = am;
       }
+      ++r;
+      ++k;
     }
     return;
   }
-  // phase 1: packed (thread, bit) codes + per-word side data
+  // phase 1: packed (word, bit) codes (+ the cell's antenna mask) and per-word side data in LDS
   {
     unsigned long long mm = m;
     int o = loc;
     while (mm) {
       const int b = __ffsll((long long)mm) - 1;
       mm &= mm - 1;
-      pk[o++] = ((unsigned)t << 6) | (unsigned)b;
+      pk[o] = ((unsigned)t << 6) | (unsigned)b;
+      if (!entries) {
+        unsigned am = 0;
+#pragma unroll
+        for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
+        pam[o] = am;
+      }
+      ++o;
     }
   }
   s_loc[t] = loc;
-  if (entries && m) {
-    const long long fa = row / S;
-    const int i = (int)(row - fa * S);
-    const long long f = fa / A;
-    int r = 0;
-    int c = (int)(cell_base[f] + cell_row_off[f * S + i]);
-    const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww)
-      if (ww < w) {
-        r += __popcll(mask[row * W + ww]);
-        c += __popcll(urow[ww]);
-      }
-    s_r0[t] = r;
-    s_cw[t] = c;
-    s_u[t] = urow[w];
-  }
+  s_r0[t] = r0;
+  s_cw[t] = cw;
+  s_u[t] = u;
+  s_fi[t] = entries ? ((a << 16) | i) : (int)f;
   __syncthreads();
   const long long first = s_first;
-  // phase 2: coalesced stores, lane k % 256 writes item k
+  const long long gw0 = gw - t;  // first word of the block
+  // phase 2: coalesced stores, lane k % 256 writes item k (no divisions: per-word data come from LDS)
   for (int k = t; k < total; k += 256) {
     const unsigned code = pk[k];
     const int tt = (int)(code >> 6), b = (int)(code & 63);
-    const long long g2 = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256 + tt;
-    const long long rw = g2 / W;
-    const int ww = (int)(g2 - rw * W);
+    const long long g2 = gw0 + tt;
+    const int ww = (int)(g2 % W);
     const long long e = first + k;
     if (entries) {
       if (e < entry_cap) {
-        const long long fa = rw / S;
-        const int i = (int)(rw - fa * S);
-        const long long f = fa / A;
+        const int ai = s_fi[tt];
+        const int ii = ai & 0xffff;
         const int r = s_r0[tt] + (k - s_loc[tt]);
-        e_ant[e] = (int)(fa - f * A);
-        e_rbin[e] = i;
+        e_ant[e] = ai >> 16;
+        e_rbin[e] = ii;
         e_dbin[e] = ww * 64 + b;
         e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
-        if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)rw * C + r] + 1e-12f));  // dechirp.py:235-236
+        if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)(g2 / W) * C + r] + 1e-12f));  // dechirp.py:235-236
       }
     } else if (e < cell_cap) {
-      const long long f = rw / S;
-      const int i = (int)(rw - f * S);
-      unsigned am = 0;
-#pragma unroll
-      for (int a = 0; a < MAXA; ++a)
-        if (a < A) am |= (unsigned)((mask[(((size_t)f * A + a) * S + i) * W + ww] >> b) & 1ull) << a;
-      c_frame[e] = (int)f;
-      c_rc[e] = i * C + ww * 64 + b;
-      c_amask[e] = am;
+      const long long rw = g2 / W;
+      c_frame[e] = s_fi[tt];
+      c_rc[e] = (int)(rw - (long long)s_fi[tt] * S) * C + ww * 64 + b;
+      c_amask[e] = pam[k];
     }
   }
 }
