@@ -175,6 +175,27 @@ int rsl_phase_model(rsl_handle h, const void* pos, const void* ang, long long n,
 int rsl_bvls(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int nv,
              double ridge, const void* lo, const void* hi, void* out);
 
+/* a30  ImprovedVelocitySolver.associate_targets_across_frames (velocity_solver_improved.py:74-129): for each
+ *     current target in order, the nearest unused previous target with Euclidean distance < thr (ties to the
+ *     lowest index).  cur_xy f64 [nc][2], prev_xy f64 [np][2] (device), scratch u32 [ceil(np/32)],
+ *     match i32 [nc] (-1 = none), dist f64 [nc]. */
+int rsl_associate(rsl_handle h, const void* cur_xy, int nc, const void* prev_xy, int np, double thr, void* scratch,
+                  void* match, void* dist);
+
+/* a30, a31  wrapped-phase ego-motion solve: minimises sum_i wrap(y_i - k J_i.x)^2 + R(x) over the box
+ *     [lo6, hi6] (host), J_i = [d_i, p_i x d_i] from pos f64 [n][3] and ang f64 [n][2] (az, el).
+ *     mode 0: R = 0.01 |v|^2 + 0.01 |w|^2 (velocity_solver_improved.py:223-266);
+ *     mode 1: the piecewise penalties of advanced_velocity_optimization.py:153-223 with weight w, max
+ *             velocity vmax, max angular velocity wmax and previous motion prev f64 [6] (device, nullable).
+ *     nv = 3 (w fixed at 0; step 1) or 6.  Multi-start projected Gauss-Newton from a grid_n x grid_n grid
+ *     over (v_x, v_y) plus nextra extra starts extra f64 [nextra][6] (device), iters iterations each;
+ *     out f64 [8] (device) = {x[6], cost, start index}.  scratch >= rsl_wrapped_scratch_bytes(n, grid_n, nextra). */
+long long rsl_wrapped_scratch_bytes(long long n, int grid_n, int nextra);
+int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int mode,
+                      double w, double vmax, double wmax, const void* prev, const double* lo6, const double* hi6,
+                      int nv, int grid_n, const void* extra, int nextra, int iters, void* scratch,
+                      long long scratch_bytes, void* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -451,6 +451,70 @@ def solve_velocity_de(solver_cls_kwargs, targets, dt=0.1):
 
 
 # ----------------------------------------------------------------------------------------
+# L3: wrapped-phase solvers (src/algorithms/velocity_solver_improved.py, advanced_velocity_optimization.py)
+# ----------------------------------------------------------------------------------------
+def associate_greedy(cur_xy, prev_xy, thr=5.0):
+    """velocity_solver_improved.py:96-126: cdist, then for each current target in order the nearest unused
+    previous target with distance < thr (strict '<' keeps the first of equal distances).
+    Returns (match [Nc] with -1 = none, dist [Nc])."""
+    from scipy.spatial.distance import cdist
+    cur = np.asarray(cur_xy, np.float64).reshape(-1, 2)
+    prev = np.asarray(prev_xy, np.float64).reshape(-1, 2)
+    D = cdist(cur, prev)
+    used = set()
+    match = np.full(len(cur), -1, np.int64)
+    dist = np.full(len(cur), np.inf)
+    for i in range(len(cur)):
+        bj, bd = None, float('inf')
+        for j in range(len(prev)):
+            if j in used:
+                continue
+            d = D[i, j]
+            if d < thr and d < bd:
+                bd, bj = d, j
+        if bj is not None:
+            used.add(bj)
+            match[i], dist[i] = bj, bd
+    return match, dist
+
+
+def phase_pred(x6, pos, ang, k):
+    """k (v + w x p).d, d = (cos el cos az, cos el sin az, sin el) (velocity_solver_improved.py:173-221)."""
+    az, el = ang[:, 0], ang[:, 1]
+    d = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=1)
+    rel = x6[:3][None, :] + np.cross(x6[3:][None, :], pos)
+    return k * np.sum(rel * d, axis=1)
+
+
+def improved_cost(x6, pos, ang, y, k):
+    """velocity_solver_improved.py:223-266: sum wrap(y - pred)^2 + 0.01 |v|^2 + 0.01 |w|^2."""
+    x6 = np.asarray(x6, np.float64)
+    r = y - phase_pred(x6, pos, ang, k)
+    r = np.arctan2(np.sin(r), np.cos(r))
+    return float(np.sum(r ** 2) + 0.01 * np.sum(x6[:3] ** 2) + 0.01 * np.sum(x6[3:] ** 2))
+
+
+def advanced_cost(x6, pos, ang, y, k, previous_motion=None, w=0.01, vmax=50.0, wmax=10.0):
+    """advanced_velocity_optimization.py:153-223 (wrapped base cost + penalties 1-5)."""
+    x6 = np.asarray(x6, np.float64)
+    r = y - phase_pred(x6, pos, ang, k)
+    r = np.arctan2(np.sin(r), np.cos(r))
+    c = float(np.sum(r ** 2))
+    vm, wm = np.linalg.norm(x6[:3]), np.linalg.norm(x6[3:])
+    reg = 0.0
+    if vm > vmax * 0.8:
+        reg += w * (vm - vmax * 0.8) ** 2
+    if wm > wmax * 0.8:
+        reg += w * (wm - wmax * 0.8) ** 2
+    if previous_motion is not None:
+        reg += w * 0.1 * np.sum((x6 - previous_motion) ** 2)
+    if vm > 20 and wm > 5:
+        reg += w * 0.01 * (vm - 20) * (wm - 5)
+    reg += w * 10.0 * x6[2] ** 2
+    return c + reg
+
+
+# ----------------------------------------------------------------------------------------
 # L4: pose integration (src/pose_integration/pose_integration.py)
 # ----------------------------------------------------------------------------------------
 def integrate_positions(vel, ts, p0=(0, 0, 0), method='trapezoidal', smoothing=True, window=5):

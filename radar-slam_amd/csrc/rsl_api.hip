@@ -496,3 +496,43 @@ int rsl_bvls(rsl_handle h, const void* pos, const void* ang, long long n, const 
 }
 
 }  // extern "C"
+
+int rsl_associate(rsl_handle h, const void* cur_xy, int nc, const void* prev_xy, int np, double thr, void* scratch,
+                  void* match, void* dist) {
+  if (!h) return RSL_ERR_INVALID;
+  if (nc < 0 || np < 0 || !(thr >= 0)) return fail(h, RSL_ERR_INVALID, "rsl_associate: bad argument");
+  if (nc > 0 && (!cur_xy || !match || !dist || (np > 0 && (!prev_xy || !scratch))))
+    return fail(h, RSL_ERR_INVALID, "rsl_associate: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_associate(h->stream, (const double*)cur_xy, nc, (const double*)prev_xy, np, thr,
+                                         (unsigned*)scratch, (int*)match, (double*)dist),
+                   "associate");
+}
+
+long long rsl_wrapped_scratch_bytes(long long n, int grid_n, int nextra) {
+  if (n < 0 || grid_n < 0 || nextra < 0) return -1;
+  return 8LL * (6 * n + 36 + 8 * ((long long)grid_n * grid_n + nextra));
+}
+
+int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int mode,
+                      double w, double vmax, double wmax, const void* prev, const double* lo6, const double* hi6,
+                      int nv, int grid_n, const void* extra, int nextra, int iters, void* scratch,
+                      long long scratch_bytes, void* out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 1 || (nv != 3 && nv != 6) || (mode != 0 && mode != 1) || grid_n < 0 || nextra < 0 || iters < 0 ||
+      grid_n * (long long)grid_n + nextra < 1)
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_solve: bad argument");
+  if (!pos || !ang || !y || !lo6 || !hi6 || !scratch || !out || (nextra > 0 && !extra))
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_solve: null pointer");
+  for (int a = 0; a < 6; ++a)
+    if (!(lo6[a] <= hi6[a])) return fail(h, RSL_ERR_INVALID, "rsl_wrapped_solve: bad bounds");
+  if (scratch_bytes < rsl_wrapped_scratch_bytes(n, grid_n, nextra))
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_solve: scratch too small");
+  Scope sc(h, RSL_K_VELOCITY);
+  return hip_check(h,
+                   rsl::launch_wrapped_solve(h->stream, (const double*)pos, (const double*)ang, n, (const double*)y,
+                                             k, mode, w, vmax, wmax, (const double*)prev, lo6, hi6, nv, grid_n,
+                                             (const double*)extra, nextra, iters, (double*)scratch, (double*)out),
+                   "wrapped_solve");
+}

@@ -67,6 +67,14 @@ hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, co
                            const double* y, const unsigned* amask, const long long* seg, int F, double k, double ridge,
                            const double* bounds4, double* out, double* resid, double* pred);
 
+// K9: greedy association and wrapped-phase multi-start solve (rsl_wrap.hip).
+hipError_t launch_associate(hipStream_t st, const double* cur, int nc, const double* prev, int np, double thr,
+                            unsigned* used_scratch, int* match, double* dist);
+hipError_t launch_wrapped_solve(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
+                                double k, int mode, double w, double vmax, double wmax, const double* prev,
+                                const double* lo, const double* hi, int nv, int gn, const double* extra, int nextra,
+                                int iters, double* scratch, double* out);
+
 }  // namespace rsl
 
 namespace rsl {

@@ -1,0 +1,386 @@
+// rsl_wrap.hip — K9: greedy cross-frame target association and the wrapped-phase (regularised) ego-motion
+// solve of the reference's "Improved" and "Advanced" solvers.  gfx950 / CDNA4, fp64 throughout.
+//
+// Replaces (reference src/algorithms/):
+//   velocity_solver_improved.py  associate_targets_across_frames :74-129, cost_function :223-266,
+//                                two_step_optimization :325-477 (differential_evolution, seed 42);
+//   advanced_velocity_optimization.py  compute_regularized_cost_function :153-223,
+//                                run_single_optimization / run_robust_optimization :343-524.
+//
+// Association: for each current target in order, the nearest not-yet-used previous target with
+// Euclidean (x, y) distance < thr (strict), ties to the lowest index — exactly the reference's greedy loop.
+// It is sequential across current targets, so one workgroup runs it per problem, with a block-wide
+// (distance, index) argmin per step.
+//
+// Wrapped solve: the cost sum_i wrap(y_i - k J_i . x)^2 + R(x), J_i = [d_i, p_i x d_i], is piecewise
+// quadratic with one basin per 2 pi / k of radial velocity (0.0195 m/s at 77 GHz, dt 0.1 s): the reference
+// runs DE over the box and reports whichever basin DE settles in.  Here every thread runs a projected
+// Gauss-Newton descent (the data Hessian 2 k^2 sum J J^T is constant, precomputed) from one start of a dense
+// (v_x, v_y) grid over the box, with backtracking on the true cost, and a reduction keeps the lowest cost.
+// Parity contract: cost <= the reference's DE cost (the argmin itself is not unique).
+#include "rsl_common.h"
+#include "rsl_internal.h"
+
+namespace rsl {
+
+// ---------------------------------------------------------------------------------------------------------
+// Greedy association (one block of 256 threads per problem).
+// ---------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_associate(const double* __restrict__ cur, int nc,
+                                                   const double* __restrict__ prev, int np, double thr,
+                                                   unsigned* __restrict__ used, int* __restrict__ match,
+                                                   double* __restrict__ dist) {
+  __shared__ double sd[256];
+  __shared__ int si[256];
+  const int t = threadIdx.x;
+  for (int j = t; j < (np + 31) / 32; j += 256) used[j] = 0u;
+  __syncthreads();
+  for (int i = 0; i < nc; ++i) {
+    const double cx = cur[2 * i], cy = cur[2 * i + 1];
+    double bd = INFINITY;
+    int bj = -1;
+    for (int j = t; j < np; j += 256) {
+      if ((used[j >> 5] >> (j & 31)) & 1u) continue;
+      const double dx = cx - prev[2 * j], dy = cy - prev[2 * j + 1];
+      const double d = sqrt(dx * dx + dy * dy);  // scipy cdist 'euclidean'
+      if (d < thr && d < bd) {  // strict: the first (lowest) j wins ties within the thread's stripe
+        bd = d;
+        bj = j;
+      }
+    }
+    sd[t] = bd;
+    si[t] = bj;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (t < off) {
+        const double od = sd[t + off];
+        const int oj = si[t + off];
+        if (oj >= 0 && (si[t] < 0 || od < sd[t] || (od == sd[t] && oj < si[t]))) {
+          sd[t] = od;
+          si[t] = oj;
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const int j = si[0];
+      match[i] = j;
+      dist[i] = j >= 0 ? sd[0] : INFINITY;
+      if (j >= 0) used[j >> 5] |= 1u << (j & 31);
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_associate(hipStream_t st, const double* cur, int nc, const double* prev, int np, double thr,
+                            unsigned* used_scratch, int* match, double* dist) {
+  if (nc <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_associate, dim3(1), dim3(256), 0, st, cur, nc, prev, np, thr, used_scratch, match, dist);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Wrapped multi-start solve.
+// ---------------------------------------------------------------------------------------------------------
+constexpr double kPi = 3.14159265358979323846;
+
+// np.arctan2(np.sin(r), np.cos(r)): r reduced to [-pi, pi]
+RSL_DEV double wrap_pi(double r) { return r - 2.0 * kPi * rint(r * (0.5 / kPi)); }
+
+struct WrapProblem {
+  const double* J;  // [N][6] = [d, p x d]
+  const double* y;  // [N]
+  long n;
+  double k;
+  int mode;         // 0 = Improved (0.01 |v|^2 + 0.01 |w|^2), 1 = Advanced (piecewise penalties)
+  double w, vmax, wmax;
+  const double* prev;  // [6] or null (Advanced temporal term)
+  double lo[6], hi[6];
+  int nv;           // 3: w fixed at 0, 6: full
+};
+
+// R(x) of the reference cost functions (exactly the reference's formulas).
+RSL_DEV double reg_cost(const WrapProblem& P, const double* x) {
+  if (P.mode == 0) {  // velocity_solver_improved.py:258-262
+    double s = 0.0, s2 = 0.0;
+    for (int a = 0; a < 3; ++a) s += x[a] * x[a];
+    for (int a = 3; a < 6; ++a) s2 += x[a] * x[a];
+    return 0.01 * s + 0.01 * s2;
+  }
+  // advanced_velocity_optimization.py:190-219
+  const double vm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  const double wm = sqrt(x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
+  double r = 0.0;
+  if (vm > P.vmax * 0.8) r += P.w * (vm - P.vmax * 0.8) * (vm - P.vmax * 0.8);
+  if (wm > P.wmax * 0.8) r += P.w * (wm - P.wmax * 0.8) * (wm - P.wmax * 0.8);
+  if (P.prev) {
+    double s = 0.0;
+    for (int a = 0; a < 6; ++a) s += (x[a] - P.prev[a]) * (x[a] - P.prev[a]);
+    r += P.w * 0.1 * s;
+  }
+  if (vm > 20 && wm > 5) r += P.w * 0.01 * ((vm - 20) * (wm - 5));
+  r += P.w * 10.0 * (x[2] * x[2]);
+  return r;
+}
+
+// Gradient and a positive semi-definite (Gauss-Newton) Hessian of R.
+RSL_DEV void reg_grad_hess(const WrapProblem& P, const double* x, double* g, double (*H)[6]) {
+  for (int a = 0; a < 6; ++a) {
+    g[a] = 0.0;
+    for (int b = 0; b < 6; ++b) H[a][b] = 0.0;
+  }
+  if (P.mode == 0) {
+    for (int a = 0; a < 6; ++a) {
+      g[a] = 0.02 * x[a];
+      H[a][a] = 0.02;
+    }
+    return;
+  }
+  const double vm = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  const double wm = sqrt(x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
+  const double av = P.vmax * 0.8, aw = P.wmax * 0.8;
+  if (vm > av) {
+    const double c = 2.0 * P.w * (vm - av) / vm;
+    for (int a = 0; a < 3; ++a) {
+      g[a] += c * x[a];
+      for (int b = 0; b < 3; ++b) H[a][b] += 2.0 * P.w * x[a] * x[b] / (vm * vm);
+    }
+  }
+  if (wm > aw) {
+    const double c = 2.0 * P.w * (wm - aw) / wm;
+    for (int a = 3; a < 6; ++a) {
+      g[a] += c * x[a];
+      for (int b = 3; b < 6; ++b) H[a][b] += 2.0 * P.w * x[a] * x[b] / (wm * wm);
+    }
+  }
+  if (P.prev) {
+    for (int a = 0; a < 6; ++a) {
+      g[a] += 0.2 * P.w * (x[a] - P.prev[a]);
+      H[a][a] += 0.2 * P.w;
+    }
+  }
+  if (vm > 20 && wm > 5) {
+    for (int a = 0; a < 3; ++a) g[a] += P.w * 0.01 * (wm - 5) * x[a] / vm;
+    for (int a = 3; a < 6; ++a) g[a] += P.w * 0.01 * (vm - 20) * x[a] / wm;
+  }
+  g[2] += 20.0 * P.w * x[2];
+  H[2][2] += 20.0 * P.w;
+}
+
+RSL_DEV double data_cost(const WrapProblem& P, const double* x, double* g /* nullable: -2k sum J r */) {
+  double c = 0.0;
+  double gg[6] = {0, 0, 0, 0, 0, 0};
+  for (long i = 0; i < P.n; ++i) {
+    const double* Ji = P.J + 6 * i;
+    double pred = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) pred += Ji[a] * x[a];
+    const double r = wrap_pi(P.y[i] - P.k * pred);
+    c += r * r;
+    if (g) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) gg[a] += Ji[a] * r;
+    }
+  }
+  if (g)
+    for (int a = 0; a < 6; ++a) g[a] = -2.0 * P.k * gg[a];
+  return c;
+}
+
+// Solve H d = -g on the first nv coordinates (Cholesky with a tiny diagonal floor), d[nv..5] = 0.
+RSL_DEV void newton_step(const double (*H)[6], const double* g, int nv, double* d) {
+  double L[6][6];
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b) L[a][b] = 0.0;
+  for (int a = 0; a < nv; ++a) {
+    for (int b = 0; b <= a; ++b) {
+      double s = H[a][b];
+      for (int q = 0; q < b; ++q) s -= L[a][q] * L[b][q];
+      if (a == b) {
+        L[a][a] = sqrt(s > 1e-12 ? s : 1e-12);
+      } else {
+        L[a][b] = s / L[b][b];
+      }
+    }
+  }
+  double z[6];
+  for (int a = 0; a < nv; ++a) {
+    double s = -g[a];
+    for (int q = 0; q < a; ++q) s -= L[a][q] * z[q];
+    z[a] = s / L[a][a];
+  }
+  for (int a = nv - 1; a >= 0; --a) {
+    double s = z[a];
+    for (int q = a + 1; q < nv; ++q) s -= L[q][a] * d[q];
+    d[a] = s / L[a][a];
+  }
+  for (int a = nv; a < 6; ++a) d[a] = 0.0;
+}
+
+// One start per thread: x0 = (grid v_x, grid v_y, extra / 0 ...), projected Gauss-Newton with backtracking.
+__global__ __launch_bounds__(256) void k_wrapped_ms(WrapProblem P, const double* __restrict__ Hd /* 6x6 */,
+                                                    int gn, const double* __restrict__ extra, int nextra,
+                                                    int iters, double* __restrict__ out /* [nstart][8] */) {
+  const long s = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nstart = (long)gn * gn + nextra;
+  if (s >= nstart) return;
+  double x[6] = {0, 0, 0, 0, 0, 0};
+  if (s < (long)gn * gn) {
+    const int ix = (int)(s % gn), iy = (int)(s / gn);
+    x[0] = P.lo[0] + (P.hi[0] - P.lo[0]) * (ix + 0.5) / gn;
+    x[1] = P.lo[1] + (P.hi[1] - P.lo[1]) * (iy + 0.5) / gn;
+  } else {
+    for (int a = 0; a < 6; ++a) x[a] = extra[(s - (long)gn * gn) * 6 + a];
+  }
+  for (int a = 0; a < 6; ++a) {
+    if (a >= P.nv) x[a] = 0.0;
+    x[a] = fmin(fmax(x[a], P.lo[a]), P.hi[a]);
+  }
+  double g[6], H[6][6], d[6], xn[6];
+  double f = data_cost(P, x, g) + reg_cost(P, x);
+  for (int it = 0; it < iters; ++it) {
+    double gr[6];
+    reg_grad_hess(P, x, gr, H);
+    for (int a = 0; a < 6; ++a) {
+      g[a] += gr[a];
+      for (int b = 0; b < 6; ++b) H[a][b] += Hd[a * 6 + b];
+    }
+    newton_step(H, g, P.nv, d);
+    double step = 1.0, fn = f;
+    bool ok = false;
+    for (int ls = 0; ls < 6; ++ls) {
+      for (int a = 0; a < 6; ++a) xn[a] = fmin(fmax(x[a] + step * d[a], P.lo[a]), P.hi[a]);
+      fn = data_cost(P, xn, nullptr) + reg_cost(P, xn);
+      if (fn < f) {
+        ok = true;
+        break;
+      }
+      step *= 0.5;
+    }
+    if (!ok) break;
+    const double df = f - fn;
+    for (int a = 0; a < 6; ++a) x[a] = xn[a];
+    f = fn;
+    if (df <= 1e-13 * (1.0 + f)) break;
+    data_cost(P, x, g);  // gradient at the new point
+  }
+  double* o = out + s * 8;
+  for (int a = 0; a < 6; ++a) o[a] = x[a];
+  o[6] = f;
+  o[7] = (double)s;
+}
+
+// Argmin over starts (lowest cost, then lowest start index): one block.
+__global__ __launch_bounds__(1024) void k_wrapped_best(const double* __restrict__ res, long nstart,
+                                                      double* __restrict__ best) {
+  __shared__ double sc[1024];
+  __shared__ long si[1024];
+  const int t = threadIdx.x;
+  double bc = INFINITY;
+  long bi = -1;
+  for (long s = t; s < nstart; s += 1024) {
+    const double c = res[s * 8 + 6];
+    if (c < bc) {
+      bc = c;
+      bi = s;
+    }
+  }
+  sc[t] = bc;
+  si[t] = bi;
+  __syncthreads();
+  for (int off = 512; off > 0; off >>= 1) {
+    if (t < off) {
+      const double oc = sc[t + off];
+      const long oi = si[t + off];
+      if (oi >= 0 && (si[t] < 0 || oc < sc[t] || (oc == sc[t] && oi < si[t]))) {
+        sc[t] = oc;
+        si[t] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const long b = si[0];
+    for (int a = 0; a < 8; ++a) best[a] = b >= 0 ? res[b * 8 + a] : 0.0;
+  }
+}
+
+// Data Hessian 2 k^2 sum J J^T (fp64), one block.
+__global__ __launch_bounds__(256) void k_wrapped_hess(const double* __restrict__ J, long n, double k,
+                                                      double* __restrict__ Hd) {
+  __shared__ double part[256][21];
+  const int t = threadIdx.x;
+  double acc[21];
+  for (int q = 0; q < 21; ++q) acc[q] = 0.0;
+  for (long i = t; i < n; i += 256) {
+    const double* Ji = J + 6 * i;
+    int q = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int b = 0; b <= a; ++b) acc[q++] += Ji[a] * Ji[b];
+  }
+  for (int q = 0; q < 21; ++q) part[t][q] = acc[q];
+  __syncthreads();
+  if (t < 21) {
+    double s = 0.0;
+    for (int u = 0; u < 256; ++u) s += part[u][t];
+    int q = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int b = 0; b <= a; ++b, ++q)
+        if (q == t) {
+          Hd[a * 6 + b] = 2.0 * k * k * s;
+          Hd[b * 6 + a] = 2.0 * k * k * s;
+        }
+  }
+}
+
+// Jacobian rows J_i = [d_i, p_i x d_i], d = (cos el cos az, cos el sin az, sin el)  (velocity_solver.py:94-109).
+__global__ __launch_bounds__(256) void k_wrapped_jac(const double* __restrict__ pos, const double* __restrict__ ang,
+                                                     long n, double* __restrict__ J) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double az = ang[2 * i], el = ang[2 * i + 1];
+  const double ce = cos(el);
+  const double d0 = ce * cos(az), d1 = ce * sin(az), d2 = sin(el);
+  const double px = pos[3 * i], py = pos[3 * i + 1], pz = pos[3 * i + 2];
+  double* o = J + 6 * i;
+  o[0] = d0;
+  o[1] = d1;
+  o[2] = d2;
+  o[3] = py * d2 - pz * d1;  // (w x p).d = w.(p x d)
+  o[4] = pz * d0 - px * d2;
+  o[5] = px * d1 - py * d0;
+}
+
+hipError_t launch_wrapped_solve(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
+                                double k, int mode, double w, double vmax, double wmax, const double* prev,
+                                const double* lo, const double* hi, int nv, int gn, const double* extra, int nextra,
+                                int iters, double* scratch, double* out) {
+  // scratch: J [6n] | Hd [36] | per-start results [8 * (gn^2 + nextra)]
+  double* J = scratch;
+  double* Hd = J + 6 * n;
+  double* res = Hd + 36;
+  hipLaunchKernelGGL(k_wrapped_jac, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos, ang, n, J);
+  hipLaunchKernelGGL(k_wrapped_hess, dim3(1), dim3(256), 0, st, J, n, k, Hd);
+  WrapProblem P;
+  P.J = J;
+  P.y = y;
+  P.n = n;
+  P.k = k;
+  P.mode = mode;
+  P.w = w;
+  P.vmax = vmax;
+  P.wmax = wmax;
+  P.prev = prev;
+  for (int a = 0; a < 6; ++a) {
+    P.lo[a] = lo[a];
+    P.hi[a] = hi[a];
+  }
+  P.nv = nv;
+  const long nstart = (long)gn * gn + nextra;
+  hipLaunchKernelGGL(k_wrapped_ms, dim3((unsigned)((nstart + 255) / 256)), dim3(256), 0, st, P, Hd, gn, extra, nextra,
+                     iters, res);
+  hipLaunchKernelGGL(k_wrapped_best, dim3(1), dim3(1024), 0, st, res, nstart, out);
+  return hipGetLastError();
+}
+
+}  // namespace rsl

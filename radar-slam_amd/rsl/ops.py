@@ -214,3 +214,54 @@ def bvls(pos, ang, y, k, lo, hi, ridge=0.0, ctx: Optional[Context] = None):
                            _ptr(out)), 'rsl_bvls')
     o = to_host(out)
     return o[:nv], float(o[nv])
+
+
+# -- a30 / a31: cross-frame association and wrapped-phase solve ------------------------------------------
+def associate(cur_xy, prev_xy, thr: float, ctx: Optional[Context] = None):
+    """Greedy nearest-unused association (velocity_solver_improved.py:74-129) on the device.
+    Returns (match int64 [Nc] with -1 for none, dist float64 [Nc])."""
+    c = _ctx(ctx)
+    torch = c.torch
+    cur = np.ascontiguousarray(np.asarray(cur_xy, np.float64).reshape(-1, 2))
+    prev = np.ascontiguousarray(np.asarray(prev_xy, np.float64).reshape(-1, 2))
+    nc, npv = cur.shape[0], prev.shape[0]
+    if nc == 0:
+        return np.zeros(0, np.int64), np.zeros(0)
+    dc = c.to_dev(cur.reshape(-1))
+    dp = c.to_dev(prev.reshape(-1)) if npv else None
+    scratch = c.empty((max((npv + 31) // 32, 1),), torch.int32)
+    match = c.empty((nc,), torch.int32)
+    dist = c.empty((nc,), torch.float64)
+    c._bind()
+    c.check(c.lib.rsl_associate(c.h, _ptr(dc), nc, _ptr(dp), npv, float(thr), _ptr(scratch), _ptr(match), _ptr(dist)),
+            'rsl_associate')
+    return to_host(match).astype(np.int64), to_host(dist)
+
+
+def wrapped_solve(pos, ang, y, k, *, mode: int, lo, hi, nv: int = 6, w: float = 0.01, vmax: float = 50.0,
+                  wmax: float = 10.0, prev=None, extra=None, grid_n: int = 512, iters: int = 12,
+                  ctx: Optional[Context] = None):
+    """Global minimisation of the wrapped-phase cost (rsl_wrapped_solve): mode 0 = Improved regularisation,
+    mode 1 = Advanced penalties.  Returns (x6, cost)."""
+    from ctypes import c_double
+    c = _ctx(ctx)
+    torch = c.torch
+    pos = np.ascontiguousarray(np.asarray(pos, np.float64).reshape(-1, 3))
+    ang = np.ascontiguousarray(np.asarray(ang, np.float64).reshape(-1, 2))
+    n = pos.shape[0]
+    ex = None if extra is None else np.ascontiguousarray(np.asarray(extra, np.float64).reshape(-1, 6))
+    nextra = 0 if ex is None else ex.shape[0]
+    nbytes = int(c.lib.rsl_wrapped_scratch_bytes(n, grid_n, nextra))
+    scratch = c.empty(((nbytes + 7) // 8,), torch.float64)
+    dp, da, dy = c.to_dev(pos.reshape(-1)), c.to_dev(ang.reshape(-1)), c.to_dev(np.asarray(y, np.float64))
+    dprev = c.to_dev(np.asarray(prev, np.float64).reshape(6)) if prev is not None else None
+    dex = c.to_dev(ex.reshape(-1)) if nextra else None
+    out = c.empty((8,), torch.float64)
+    lo6 = (c_double * 6)(*[float(v) for v in lo])
+    hi6 = (c_double * 6)(*[float(v) for v in hi])
+    c._bind()
+    c.check(c.lib.rsl_wrapped_solve(c.h, _ptr(dp), _ptr(da), n, _ptr(dy), float(k), int(mode), float(w), float(vmax),
+                                    float(wmax), _ptr(dprev), lo6, hi6, int(nv), int(grid_n), _ptr(dex), nextra,
+                                    int(iters), _ptr(scratch), nbytes, _ptr(out)), 'rsl_wrapped_solve')
+    o = to_host(out)
+    return o[:6].copy(), float(o[6])

@@ -1,0 +1,210 @@
+"""Improved two-step ego-velocity solve (temporal phase differences + cross-frame association) on MI355X.
+
+Drop-in for ``src/algorithms/velocity_solver_improved.py`` of the reference (``ImprovedVelocitySolver``
+:25-506): same constructor, attributes, methods, return types and dict keys.
+
+Device work (librsl):
+* ``associate_targets_across_frames`` -> ``rsl_associate``: the reference's greedy loop (for each current
+  target in order, the nearest unused previous target closer than ``association_threshold``, :104-126),
+  one workgroup with a block-wide (distance, index) argmin per step;
+* ``cost_function`` / ``compute_phase_difference_model`` -> ``rsl_phase_model`` (wrapped residuals, ridge 0.01);
+* ``two_step_optimization`` -> ``rsl_wrapped_solve`` (mode 0).  The reference minimises the wrapped,
+  regularised cost (:223-266) with differential evolution (seed 42, :387-396 and :421-430).  That cost has one
+  basin per 2 pi / k of radial velocity (0.0195 m/s at 77 GHz, dt = 0.1 s), so DE's answer is one local
+  minimum among millions.  librsl runs projected Gauss-Newton from every point of a dense (v_x, v_y) grid over
+  the same box (plus the initial guess) and keeps the lowest cost.  Parity contract: cost <= the reference's
+  DE cost (tests/test_gpu_wrapped.py against tests/golden/golden_wrapped.npz).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from rsl import ops
+
+logger = logging.getLogger(__name__)
+
+_TRANS_BOUNDS = [(-50, 50), (-50, 50), (-10, 10)]                           # velocity_solver_improved.py:383
+_FULL_BOUNDS = _TRANS_BOUNDS + [(-10, 10), (-10, 10), (-10, 10)]           # :417-418
+GRID_N = 512  # (v_x, v_y) start grid per solve: 262,144 Gauss-Newton descents
+
+
+def _opt_result(x, fun, nfev, method):
+    from scipy.optimize import OptimizeResult
+    return OptimizeResult(x=np.asarray(x, dtype=np.float64), fun=float(fun), success=True, status=0, nit=0,
+                          nfev=int(nfev), message=f'multi-start projected Gauss-Newton on the device ({method})')
+
+
+def _targets_xy(targets):
+    return np.array([[t['range_m'] * np.cos(t['azimuth_rad']), t['range_m'] * np.sin(t['azimuth_rad'])]
+                     for t in targets], dtype=np.float64).reshape(-1, 2)
+
+
+class ImprovedVelocitySolver:
+    """Reference constructor / attributes / methods (velocity_solver_improved.py:25-506)."""
+
+    def __init__(self, fc: float = 77e9, lambda_c: float = None, num_antennas: int = 8,
+                 antenna_spacing: float = None, optimization_method: str = 'differential_evolution',
+                 max_iterations: int = 1000, tolerance: float = 1e-6, association_threshold: float = 5.0):
+        self.fc = fc
+        self.c = 3e8
+        self.lambda_c = lambda_c or (self.c / self.fc)
+        self.num_antennas = num_antennas
+        self.antenna_spacing = antenna_spacing or (self.lambda_c / 2)
+        self.optimization_method = optimization_method
+        self.max_iterations = max_iterations
+        self.tolerance = tolerance
+        self.association_threshold = association_threshold
+        self.antenna_positions = np.arange(self.num_antennas) * self.antenna_spacing
+        logger.info("Initialized improved velocity solver:")
+        logger.info(f"  Wavelength: {self.lambda_c * 1000:.2f} mm")
+        logger.info(f"  Association threshold: {association_threshold} m")
+        logger.info(f"  Optimization method: {optimization_method}")
+
+    def _k(self, dt):
+        return 4 * np.pi * dt / self.lambda_c
+
+    # -- association (:74-129) ----------------------------------------------------------------------------
+    def associate_targets_across_frames(self, current_targets: List[Dict],
+                                        previous_targets: List[Dict]) -> List[Dict]:
+        if not previous_targets:
+            logger.warning("No previous targets for association")
+            return []
+        match, dist = ops.associate(_targets_xy(current_targets), _targets_xy(previous_targets),
+                                    self.association_threshold)
+        associations = []
+        for i, j in enumerate(match.tolist()):
+            if j < 0:
+                continue
+            cur, prev = current_targets[i], previous_targets[j]
+            associations.append({'current': cur, 'previous': prev, 'distance': float(dist[i]),
+                                 'temporal_phase_diff': self._compute_temporal_phase_difference(cur, prev)})
+        logger.info(f"Associated {len(associations)} targets across frames")
+        return associations
+
+    def _compute_temporal_phase_difference(self, current_target: Dict, previous_target: Dict) -> float:
+        """angle(s_cur[0] conj(s_prev[0])) (:131-152)."""
+        return np.angle(current_target['spatial_signature'][0] * np.conj(previous_target['spatial_signature'][0]))
+
+    def compute_observed_phase_differences(self, target_associations: List[Dict]) -> np.ndarray:
+        return np.array([a['temporal_phase_diff'] for a in target_associations])
+
+    # -- model and cost (:173-266) -------------------------------------------------------------------------
+    def compute_phase_difference_model(self, target_positions: np.ndarray, target_angles: np.ndarray,
+                                       velocity: np.ndarray, angular_velocity: np.ndarray, dt: float) -> np.ndarray:
+        x = np.concatenate([np.asarray(velocity, np.float64).reshape(3),
+                            np.asarray(angular_velocity, np.float64).reshape(3)])
+        return ops.phase_model(target_positions, target_angles, x, self._k(dt))['pred']
+
+    def cost_function(self, motion_params: np.ndarray, target_positions: np.ndarray, target_angles: np.ndarray,
+                      observed_phases: np.ndarray, dt: float) -> float:
+        """sum wrap(y - pred)^2 + 0.01 |v|^2 + 0.01 |w|^2 (:245-264)."""
+        return ops.phase_model(target_positions, target_angles, np.asarray(motion_params, np.float64), self._k(dt),
+                               y=observed_phases, wrap=True, ridge=0.01)['cost']
+
+    def get_smart_initial_guess(self, target_associations: List[Dict], dt: float) -> np.ndarray:
+        """-median apparent target velocity (:268-323)."""
+        if not target_associations:
+            return np.array([0, 0, 0, 0, 0, 0])
+        cur = _targets_xy([a['current'] for a in target_associations])
+        prev = _targets_xy([a['previous'] for a in target_associations])
+        tv = np.concatenate([(cur - prev) / dt, np.zeros((len(cur), 1))], axis=1)
+        med = np.median(tv, axis=0)
+        guess = np.concatenate([np.append(-med[:2], 0), np.array([0, 0, 0])])
+        logger.info(f"Smart initial guess: velocity={guess[:3]}, angular={guess[3:]}")
+        return guess
+
+    # -- optimisation (:325-477) ---------------------------------------------------------------------------
+    def _geometry(self, target_associations):
+        r = np.array([a['current']['range_m'] for a in target_associations], np.float64)
+        az = np.array([a['current']['azimuth_rad'] for a in target_associations], np.float64)
+        el = np.zeros_like(az)  # "Assume ground level" (:360)
+        pos = np.stack([r * np.cos(el) * np.cos(az), r * np.cos(el) * np.sin(az), r * np.sin(el)], axis=1)
+        return pos, np.stack([az, el], axis=1)
+
+    def two_step_optimization(self, target_associations: List[Dict], dt: float,
+                              initial_guess: Optional[np.ndarray] = None) -> Dict:
+        if len(target_associations) < 3:
+            logger.warning("Insufficient target associations for optimization")
+            return {'success': False, 'message': 'Insufficient target associations'}
+        pos, ang = self._geometry(target_associations)
+        observed = self.compute_observed_phase_differences(target_associations)
+        if initial_guess is None:
+            initial_guess = self.get_smart_initial_guess(target_associations, dt)
+        k = self._k(dt)
+        bounded = self.optimization_method == 'differential_evolution'
+        big = 1e6
+        tb = _TRANS_BOUNDS if bounded else [(-big, big)] * 3
+        fb = _FULL_BOUNDS if bounded else [(-big, big)] * 6
+        lo = [b[0] for b in fb]
+        hi = [b[1] for b in fb]
+        lo3 = [b[0] for b in tb] + [0, 0, 0]
+        hi3 = [b[1] for b in tb] + [0, 0, 0]
+        g0 = np.asarray(initial_guess, np.float64).reshape(6)
+        logger.info("Step 1: Solving for translational velocity...")
+        x3, c3 = ops.wrapped_solve(pos, ang, observed, k, mode=0, lo=lo3, hi=hi3, nv=3, extra=g0[None], grid_n=GRID_N)
+        logger.info(f"Step 1 result: v_trans = {x3[:3]}")
+        logger.info("Step 2: Refining with full 6-DoF motion...")
+        g1 = np.concatenate([x3[:3], [0, 0, 0]])
+        x6, c6 = ops.wrapped_solve(pos, ang, observed, k, mode=0, lo=lo, hi=hi, nv=6, extra=np.stack([g1, g0]),
+                                   grid_n=GRID_N)
+        velocity_est, angular_velocity_est = x6[:3].copy(), x6[3:].copy()
+        m = ops.phase_model(pos, ang, x6, k, y=observed, wrap=True)  # residuals wrapped as :456
+        predicted, residuals = m['pred'], m['resid']
+        rmse = np.sqrt(np.mean(residuals ** 2))
+        max_residual = np.max(np.abs(residuals))
+        nfev = GRID_N * GRID_N
+        results = {'success': True, 'velocity': velocity_est, 'angular_velocity': angular_velocity_est,
+                   'cost': c6, 'rmse': rmse, 'max_residual': max_residual, 'residuals': residuals,
+                   'predicted_phases': predicted, 'observed_phases': observed,
+                   'num_associations': len(target_associations),
+                   'step1_result': _opt_result(x3[:3], c3, nfev, 'rsl_wrapped_solve, 3 unknowns'),
+                   'step2_result': _opt_result(x6, c6, nfev, 'rsl_wrapped_solve, 6 unknowns')}
+        logger.info("Optimization complete:")
+        logger.info(f"  Velocity: {velocity_est}")
+        logger.info(f"  Angular velocity: {angular_velocity_est}")
+        logger.info(f"  RMSE: {rmse:.6f}")
+        logger.info(f"  Max residual: {max_residual:.6f}")
+        return results
+
+    def solve_velocity_with_association(self, current_targets: List[Dict], previous_targets: List[Dict],
+                                        dt: float = 0.1) -> Dict:
+        target_associations = self.associate_targets_across_frames(current_targets, previous_targets)
+        if not target_associations:
+            logger.warning("No target associations found")
+            return {'success': False, 'message': 'No target associations'}
+        return self.two_step_optimization(target_associations, dt)
+
+
+def estimate_velocity_improved(current_angles_path: str, previous_angles_path: str, output_path: str,
+                               radar_params: Dict = None, dt: float = 0.1) -> Dict:
+    """File wrapper (velocity_solver_improved.py:509-559): loads the pipeline's own angle files (object arrays
+    of target dicts written by extract_angles_from_rds), solves, saves with np.savez."""
+    current_targets = np.load(current_angles_path, allow_pickle=True)['targets']
+    previous_targets = np.load(previous_angles_path, allow_pickle=True)['targets']
+    logger.info(f"Loaded {len(current_targets)} current targets")
+    logger.info(f"Loaded {len(previous_targets)} previous targets")
+    if radar_params is None:
+        radar_params = {'fc': 77e9, 'lambda_c': 3e8 / 77e9, 'num_antennas': 8}
+    solver = ImprovedVelocitySolver(**radar_params)
+    results = solver.solve_velocity_with_association(current_targets, previous_targets, dt)
+    np.savez(output_path, **results)
+    logger.info(f"Improved velocity estimation complete: {results['success']}")
+    if results['success']:
+        logger.info(f"  Velocity: {results['velocity']}")
+        logger.info(f"  Angular velocity: {results['angular_velocity']}")
+        logger.info(f"  RMSE: {results['rmse']:.6f}")
+    return results
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser(description='Estimate velocity with improved method')
+    ap.add_argument('--current', required=True)
+    ap.add_argument('--previous', required=True)
+    ap.add_argument('--out', required=True)
+    ap.add_argument('--dt', type=float, default=0.1)
+    a = ap.parse_args()
+    print(f"Improved velocity estimation complete: {estimate_velocity_improved(a.current, a.previous, a.out, dt=a.dt)}")

@@ -14,6 +14,8 @@ MODULES = {
     'src.algorithms.robust_angle_estimation': 'src/algorithms/robust_angle_estimation.py',
     'src.robust_angle_estimation': 'src/robust_angle_estimation.py',
     'src.pose_integration.pose_integration': 'src/pose_integration/pose_integration.py',
+    'src.algorithms.velocity_solver_improved': 'src/algorithms/velocity_solver_improved.py',
+    'src.algorithms.advanced_velocity_optimization': 'src/algorithms/advanced_velocity_optimization.py',
 }
 
 
