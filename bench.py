@@ -5,9 +5,10 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One step = one pass of the full per-frame chain (configs[2]: RDS + peak detection + MUSIC DoA argmax +
-ESPRIT + least-squares velocity) over a batch of F synthetic frames already resident in HBM.  Frames
-shard across ranks (one process per GPU, weak scaling, no data-path collective); per step the per-frame
-velocities are gathered to rank 0 over RCCL (the trajectory reduction of the north star).  Rank 0
+ESPRIT + least-squares velocity + trajectory integration) over a batch of F synthetic frames already
+resident in HBM.  Frames shard across ranks (one process per GPU, weak scaling, no data-path collective);
+the only exchange is the trajectory reduction of the north star: each rank scans its block's poses on the
+device, the ranks all-gather 16-double block summaries and then the per-frame poses over RCCL/xGMI.  Rank 0
 prints one JSON line.
 """
 from __future__ import annotations
@@ -142,12 +143,13 @@ def main():
     chain = rsl.RadarChain(cfg, F, ctx)
     nb = 2
     cubes = make_cubes(torch, dev, nb, F, A, C, S, seed=1234 + 7919 * rank)
-    gather_buf = [torch.empty((F, 2), dtype=torch.float64, device=dev) for _ in range(world)] if world > 1 else None
+    # trajectory reduction: device prefix scan of this rank's frame block, all-gather of the
+    # 16-double block summaries and of the per-frame poses over RCCL/xGMI (rsl/traj.py)
+    reducer = rsl.TrajectoryReducer(ctx, F, dt=cfg.dt)
 
     def step(i):
         chain.run(cubes[i % nb])
-        if world > 1:  # trajectory reduction: per-frame (vx, vy) to every rank over RCCL/xGMI
-            dist.all_gather(gather_buf, chain.vel[:, :2].contiguous())
+        reducer.step(chain.vel, vstride=chain.vel.shape[1], nv=2)
 
     for i in range(args.warmup):
         step(i)

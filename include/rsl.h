@@ -196,6 +196,24 @@ int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long 
                       int nv, int grid_n, const void* extra, int nextra, int iters, void* scratch,
                       long long scratch_bytes, void* out);
 
+/* L4 trajectory  PoseIntegrator.integrate_translational_velocity / integrate_angular_velocity
+ *     (pose_integration.py:67-167) as block-wide fp64 prefix scans over one frame block.
+ *     vel f64 [F][vstride] (first nv <= 3 components used, missing ones 0), omega f64 [F][ostride] (nullable = 0),
+ *     timestamps f64 [F] (nullable: uniform dt); method 0 = trapezoidal, 1 = euler.
+ *     pos f64 [F][3] (pos[0] = 0), quat f64 [F][4] (w,x,y,z; quat[0] = identity),
+ *     summary f64 [16] (nullable) = {pos[F-1], quat[F-1], v[F-1], v[0], omega[F-1]} for stitching blocks. */
+int rsl_traj_scan(rsl_handle h, const void* vel, int vstride, int nv, const void* omega, int ostride,
+                  const void* timestamps, double dt, long long F, int method, void* pos, void* quat, void* summary);
+/* Stitch: pos[i] += base[0:3], quat[i] = base[3:7] (x) quat[i]; base f64 [7] (device). */
+int rsl_traj_apply(rsl_handle h, void* pos, void* quat, long long F, const void* base);
+/* Stitch consecutive frame blocks (e.g. one per GPU after an all-gather of the 16-double summaries, rank order):
+ *     state f64 [16] (device, in/out) = {pos (3), quat (4), v_last (3), omega_last (3), started, 0, 0}, zero-init
+ *     except quat = (1,0,0,0) (plus the initial pose); base f64 [7] (device, out) = offset of block `rank`. */
+int rsl_traj_stitch(rsl_handle h, const void* summaries, int R, int rank, double dt, int method, void* state,
+                    void* base);
+/* uniform_filter1d(x[:, c], size, mode='nearest') per column (pose_integration.py:105-109); x, out f64 [F][ncol]. */
+int rsl_traj_smooth(rsl_handle h, const void* x, long long F, int ncol, int size, void* out);
+
 #ifdef __cplusplus
 }
 #endif

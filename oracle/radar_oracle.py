@@ -535,3 +535,22 @@ def integrate_positions(vel, ts, p0=(0, 0, 0), method='trapezoidal', smoothing=T
         for i in range(3):
             pos[:, i] = uniform_filter1d(pos[:, i], size=window, mode='nearest')
     return pos
+
+
+def integrate_rotations(om, ts, r0=None):
+    """pose_integration.py:113-167: R_i = R_{i-1} * from_rotvec(axis * |w_{i-1}| dt_{i-1}) when |w| > 1e-12.
+    Returns rotation matrices [N, 3, 3]."""
+    from scipy.spatial.transform import Rotation
+    N = len(om)
+    rot = np.zeros((N, 3, 3))
+    rot[0] = np.eye(3) if r0 is None else r0
+    dt = np.diff(ts)
+    for i in range(1, N):
+        w = om[i - 1]
+        m = np.linalg.norm(w)
+        if m > 1e-12:
+            inc = Rotation.from_rotvec(w / m * (m * dt[i - 1]))
+            rot[i] = (Rotation.from_matrix(rot[i - 1]) * inc).as_matrix()
+        else:
+            rot[i] = rot[i - 1]
+    return rot

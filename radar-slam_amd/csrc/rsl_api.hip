@@ -536,3 +536,46 @@ int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long 
                                              (const double*)extra, nextra, iters, (double*)scratch, (double*)out),
                    "wrapped_solve");
 }
+
+int rsl_traj_scan(rsl_handle h, const void* vel, int vstride, int nv, const void* omega, int ostride,
+                  const void* timestamps, double dt, long long F, int method, void* pos, void* quat, void* summary) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || nv < 0 || nv > 3 || vstride < nv || (omega && ostride < 3) || (method != 0 && method != 1))
+    return fail(h, RSL_ERR_INVALID, "rsl_traj_scan: bad argument");
+  if (F > 0 && (!vel || !pos || !quat)) return fail(h, RSL_ERR_INVALID, "rsl_traj_scan: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_traj_scan(h->stream, (const double*)vel, vstride, nv, (const double*)omega, ostride,
+                                         (const double*)timestamps, dt, F, method, (double*)pos, (double*)quat,
+                                         (double*)summary),
+                   "traj_scan");
+}
+
+int rsl_traj_apply(rsl_handle h, void* pos, void* quat, long long F, const void* base) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || (F > 0 && (!pos || !quat || !base))) return fail(h, RSL_ERR_INVALID, "rsl_traj_apply: bad argument");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h, rsl::launch_traj_apply(h->stream, (double*)pos, (double*)quat, F, (const double*)base),
+                   "traj_apply");
+}
+
+int rsl_traj_smooth(rsl_handle h, const void* x, long long F, int ncol, int size, void* out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || ncol < 1 || size < 1 || (F > 0 && (!x || !out)))
+    return fail(h, RSL_ERR_INVALID, "rsl_traj_smooth: bad argument");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h, rsl::launch_traj_smooth(h->stream, (const double*)x, F, ncol, size, (double*)out),
+                   "traj_smooth");
+}
+
+int rsl_traj_stitch(rsl_handle h, const void* summaries, int R, int rank, double dt, int method, void* state,
+                    void* base) {
+  if (!h) return RSL_ERR_INVALID;
+  if (R < 1 || rank < 0 || rank >= R || (method != 0 && method != 1) || !summaries || !state || !base)
+    return fail(h, RSL_ERR_INVALID, "rsl_traj_stitch: bad argument");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_traj_stitch(h->stream, (const double*)summaries, R, rank, dt, method, (double*)state,
+                                           (double*)base),
+                   "traj_stitch");
+}

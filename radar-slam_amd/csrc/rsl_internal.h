@@ -75,6 +75,15 @@ hipError_t launch_wrapped_solve(hipStream_t st, const double* pos, const double*
                                 const double* lo, const double* hi, int nv, int gn, const double* extra, int nextra,
                                 int iters, double* scratch, double* out);
 
+// Trajectory scans (rsl_traj.hip).
+hipError_t launch_traj_scan(hipStream_t st, const double* vel, int vstride, int nv, const double* om, int ostride,
+                            const double* ts, double dt, long F, int method, double* pos, double* quat,
+                            double* summary);
+hipError_t launch_traj_apply(hipStream_t st, double* pos, double* quat, long F, const double* base);
+hipError_t launch_traj_stitch(hipStream_t st, const double* summ, int R, int rank, double dt, int method,
+                              double* state, double* base);
+hipError_t launch_traj_smooth(hipStream_t st, const double* x, long F, int ncol, int size, double* out);
+
 }  // namespace rsl
 
 namespace rsl {

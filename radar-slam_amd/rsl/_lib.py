@@ -58,6 +58,10 @@ SIGNATURES = {
     'rsl_wrapped_solve': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, c_double, c_double, _P,
                                   POINTER(c_double), POINTER(c_double), c_int, c_int, _P, c_int, c_int, _P,
                                   c_longlong, _P]),
+    'rsl_traj_scan': (c_int, [_P, _P, c_int, c_int, _P, c_int, _P, c_double, c_longlong, c_int, _P, _P, _P]),
+    'rsl_traj_apply': (c_int, [_P, _P, _P, c_longlong, _P]),
+    'rsl_traj_stitch': (c_int, [_P, _P, c_int, c_int, c_double, c_int, _P, _P]),
+    'rsl_traj_smooth': (c_int, [_P, _P, c_longlong, c_int, c_int, _P]),
     'rsl_bvls': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, _P, _P, _P]),
 }
 

@@ -1,0 +1,120 @@
+"""Trajectory reduction over frame blocks: device prefix scans per block, block
+stitching from 16-double summaries, one all-gather of the summaries and one all-gather of the poses.
+
+Reference: src/pose_integration/pose_integration.py:67-167 (trapezoidal / euler positions, rotation
+composition R_i = R_{i-1} * exp(omega_{i-1} dt)).  Each GPU integrates its own contiguous frame block with
+``rsl_traj_scan`` (positions relative to the block's first frame, orientation quaternions relative to identity),
+all ranks all-gather the block summaries over RCCL (16 doubles per rank), every rank stitches with
+``rsl_traj_stitch`` (the running state carries the pose across steps), applies its block offset with
+``rsl_traj_apply``, and the per-frame poses [F, 7] (x, y, z, qw, qx, qy, qz) are all-gathered.  The exchange
+is the only collective of the chain: latency-bound (tens of bytes), not per-link bandwidth-bound.
+
+``stitch_host`` is the same stitching rule in numpy (it runs in the gloo tests on CPU and pins the kernel).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+
+SUMMARY = 16
+STATE = 16
+
+
+def quat_mul(a, b):
+    """Hamilton product (w, x, y, z): composition as scipy's Rotation.__mul__."""
+    aw, ax, ay, az = a
+    bw, bx, by, bz = b
+    return np.array([aw * bw - ax * bx - ay * by - az * bz, aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by - ax * bz + ay * bw + az * bx, aw * bz + ax * by - ay * bx + az * bw])
+
+
+def rotvec_quat(w, dt):
+    """Rotation.from_rotvec(axis * |w| dt) with the reference's |w| > 1e-12 gate (pose_integration.py:139-151)."""
+    m = float(np.sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]))
+    if not m > 1e-12:
+        return np.array([1.0, 0.0, 0.0, 0.0])
+    s, c = np.sin(0.5 * m * dt) / m, np.cos(0.5 * m * dt)
+    return np.array([c, w[0] * s, w[1] * s, w[2] * s])
+
+
+def initial_state(p0=(0.0, 0.0, 0.0), q0=(1.0, 0.0, 0.0, 0.0)) -> np.ndarray:
+    s = np.zeros(STATE)
+    s[0:3] = p0
+    s[3:7] = q0
+    return s
+
+
+def stitch_host(summaries: np.ndarray, state: np.ndarray, rank: int, dt: float,
+                method: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """numpy mirror of k_traj_stitch: (base [7] of block `rank`, new state)."""
+    p, q = state[0:3].copy(), state[3:7].copy()
+    vl, wl, started = state[7:10].copy(), state[10:13].copy(), state[13] != 0.0
+    base = None
+    for r, s in enumerate(np.asarray(summaries).reshape(-1, SUMMARY)):
+        if started:
+            p = p + (0.5 * dt * (vl + s[10:13]) if method == 0 else dt * vl)
+            q = quat_mul(q, rotvec_quat(wl, dt))
+        if r == rank:
+            base = np.concatenate([p, q])
+        p = p + s[0:3]
+        q = quat_mul(q, s[3:7])
+        vl, wl, started = s[7:10].copy(), s[13:16].copy(), True
+    new = np.zeros(STATE)
+    new[0:3], new[3:7], new[7:10], new[10:13], new[13] = p, q, vl, wl, 1.0
+    return base, new
+
+
+class TrajectoryReducer:
+    """Per-rank device trajectory of consecutive frame blocks (one block per step per rank)."""
+
+    def __init__(self, ctx, frames: int, *, dt: float = 0.1, method: str = 'trapezoidal', group=None):
+        import torch
+        self.ctx, self.F, self.dt = ctx, int(frames), float(dt)
+        self.method = 0 if method == 'trapezoidal' else 1
+        e = ctx.empty
+        self.pos = e((self.F, 3), torch.float64)
+        self.quat = e((self.F, 4), torch.float64)
+        self.summary = e((SUMMARY,), torch.float64)
+        self.base = e((7,), torch.float64)
+        self.state = ctx.to_dev(initial_state())
+        self.group = group
+        import torch.distributed as dist
+        self.dist = dist
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.summaries = e((self.world, SUMMARY), torch.float64)
+        self.poses = e((self.F, 7), torch.float64)
+        self.all_poses = e((self.world * self.F, 7), torch.float64) if self.world > 1 else self.poses
+
+    def step(self, vel, *, vstride: int, nv: int = 2, omega=None, ostride: int = 3):
+        """vel: device f64 rows (v_x, v_y[, v_z], ...) of this rank's block; returns all ranks' poses [R*F, 7]."""
+        from .runtime import _ptr
+        c = self.ctx
+        c._bind()
+        c.check(c.lib.rsl_traj_scan(c.h, _ptr(vel), int(vstride), int(nv), _ptr(omega), int(ostride), None,
+                                    self.dt, self.F, self.method, _ptr(self.pos), _ptr(self.quat),
+                                    _ptr(self.summary)), 'rsl_traj_scan')
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(self.summaries.view(-1), self.summary, group=self.group)
+        else:
+            self.summaries[0].copy_(self.summary)
+        c._bind()
+        c.check(c.lib.rsl_traj_stitch(c.h, _ptr(self.summaries), self.world, self.rank, self.dt, self.method,
+                                      _ptr(self.state), _ptr(self.base)), 'rsl_traj_stitch')
+        c.check(c.lib.rsl_traj_apply(c.h, _ptr(self.pos), _ptr(self.quat), self.F, _ptr(self.base)), 'rsl_traj_apply')
+        self.poses[:, 0:3].copy_(self.pos)
+        self.poses[:, 3:7].copy_(self.quat)
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(self.all_poses, self.poses, group=self.group)
+        return self.all_poses
+
+
+def smooth(ctx, x, size: int = 5):
+    """uniform_filter1d(x[:, c], size, mode='nearest') per column on the device (pose_integration.py:105-109)."""
+    from .runtime import _ptr
+    F, ncol = x.shape
+    out = ctx.empty((F, ncol), x.dtype)
+    ctx._bind()
+    ctx.check(ctx.lib.rsl_traj_smooth(ctx.h, _ptr(x), F, ncol, int(size), _ptr(out)), 'rsl_traj_smooth')
+    return out
