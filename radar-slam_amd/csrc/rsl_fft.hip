@@ -7,6 +7,7 @@
 // so the kernel zeroes range bin 0 instead of reducing a mean (exact in real arithmetic).
 // conj(ref)*w is precomputed on the host in fp64 (the chirp phase reaches 2.5e7 rad) and passed as a c64 table.
 #include <cstdlib>
+#include <type_traits>
 
 #include "rsl_common.h"
 #include "rsl_internal.h"
@@ -19,7 +20,7 @@ constexpr int kThreads = 256;
 static long resident_grid(const void* kern, size_t lds, long ntile) {
   int nb = 0, dev = 0, ncu = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kThreads, lds) != hipSuccess || nb < 1) nb = 1;
-  if (nb > 4) nb = 4;
+  if (nb > 8) nb = 8;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const long g = (long)nb * ncu;
@@ -110,12 +111,11 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // and issues the next tile's 16-B global loads into registers before running the current tile's LDS FFT, so
 // HBM latency overlaps the FFT instead of stalling every tile's load phase.  Requires even S with
 // rows_for(S) * S / 2 a multiple of the block size (every power-of-two S >= 16).
-template <int S>
+template <int S, int CB>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
                                                            float2* __restrict__ work) {
-  constexpr int CB = rows_for(S);
   constexpr int LD = lp_row(S);
   constexpr int H = S / 2;                 // float4 (2 complex) per row
   constexpr int PF = CB * H / kThreads;    // float4 per thread per tile
@@ -227,14 +227,13 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-template <int C>
+template <int C, int KB>
 __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
                                                              float thr_f, int i_lo, int i_hi,
                                                              unsigned long long* __restrict__ mask,
                                                              int* __restrict__ row_count, float* __restrict__ dbmap,
                                                              float* __restrict__ pk_pow) {
-  constexpr int KB = rows_for(C);
   constexpr int NR = KB + 2;
   constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
   constexpr int W = (C + 63) / 64;
@@ -319,19 +318,49 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
   }
 }
 
-template <int C>
-static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
-                             double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
-                             float* pk_pow) {
-  constexpr int KB = rows_for(C);
+template <int C, int KB>
+static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw,
+                                float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
+                                int* row_count, float* dbmap, float* pk_pow) {
   const long ntile = (long)F * A * (S / KB);
   const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * (lp_row(C) | 1));
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
   // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
-  hipLaunchKernelGGL(k_doppler_detect<C>, dim3((unsigned)ntile), dim3(kThreads), lds, st, work, S, tw, rds, thr_f,
-                     i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+  hipLaunchKernelGGL((k_doppler_detect<C, KB>), dim3((unsigned)ntile), dim3(kThreads), lds, st, work, S, tw, rds,
+                     thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
   return hipGetLastError();
+}
+
+// range bins per Doppler/detect tile: rows_for(C), or RSL_DD_KB (16 / 32 / 64) when it tiles S/2
+static int dd_kb(int C, int S) {
+  // ~20 KiB tiles: measured fastest at C = 128 (KB 16: 2.42 ms vs KB 32: 3.23 ms per 1000 cfg2 frames; more
+  // resident workgroups hide the per-tile load -> FFT -> store phases)
+  int kb = 2048 / C < 1 ? 1 : 2048 / C;
+  if (kb > rows_for(C) || (S / 2) % kb != 0 || S % kb != 0) kb = rows_for(C);
+  if (const char* e = getenv("RSL_DD_KB")) {
+    const int v = atoi(e);
+    if ((v == 8 || v == 16 || v == 32 || v == 64) && (S / 2) % v == 0 && (size_t)(v + 2) * (lp_row(C) | 1) * 8 <= 60 * 1024)
+      kb = v;
+  }
+  return kb;
+}
+
+template <int C>
+static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
+                             double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
+                             float* pk_pow) {
+  constexpr int K0 = rows_for(C);
+  constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
+  const int kb = dd_kb(C, S);
+#define K2D(KBV) return launch_k2d_kb<C, KBV>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow)
+  if (kb == K1) K2D(K1);
+  if constexpr (C == 128) {  // tuning variants (RSL_DD_KB)
+    if (kb == 8) K2D(8);
+    if (kb == 64) K2D(64);
+  }
+  K2D(K0);
+#undef K2D
 }
 
 template <int S>
@@ -339,12 +368,22 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
                             const float2* table, const float2* tw, int dc, float2* work) {
   constexpr int CB = rows_for(S);
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
-    const long ntile = (long)F * A * ((C + CB - 1) / CB);
-    const size_t lds = sizeof(float2) * (S + (size_t)CB * lp_row(S));
-    const long nblk = resident_grid(reinterpret_cast<const void*>(k_range_fft_p<S>), lds, ntile);
-    hipLaunchKernelGGL(k_range_fft_p<S>, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile,
-                       table, tw, dc, work);
-    return hipGetLastError();
+    auto go = [&](auto cbc) -> hipError_t {
+      constexpr int CBX = decltype(cbc)::value;
+      const long ntile = (long)F * A * ((C + CBX - 1) / CBX);
+      const size_t lds = sizeof(float2) * (S + (size_t)CBX * lp_row(S));
+      const long nblk = resident_grid(reinterpret_cast<const void*>(k_range_fft_p<S, CBX>), lds, ntile);
+      hipLaunchKernelGGL((k_range_fft_p<S, CBX>), dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C,
+                         ntile, table, tw, dc, work);
+      return hipGetLastError();
+    };
+    if constexpr (S == 512) {  // RSL_RF_CB: chirp rows per tile (4 / 8 / 16) for tuning
+      const char* e = getenv("RSL_RF_CB");
+      const int v = e ? atoi(e) : CB;
+      if (v == 4) return go(std::integral_constant<int, 4>{});
+      if (v == 16) return go(std::integral_constant<int, 16>{});
+    }
+    return go(std::integral_constant<int, CB>{});
   }
   const long nblk = (long)F * A * ((C + CB - 1) / CB);
   const size_t lds = sizeof(float2) * (S + (size_t)CB * lp_row(S));
@@ -448,7 +487,7 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
 
 bool doppler_detect_supported(int C, int S) {
   if (!fft_supported(C) || (C & (C - 1)) != 0 || C < 8 || C > 1024 || (S & 1)) return false;  // LDS <= 64 KiB
-  const int KB = rows_for(C);
+  const int KB = dd_kb(C, S);
   return S % KB == 0 && (S / 2) % KB == 0;
 }
 
