@@ -19,6 +19,8 @@
 // MUSIC rule (angle_estimation.py:149-152): the spectrum is 1/(M - P) if M - P > 1e-12 else 0.  That can
 // only change the argmax when max P is within rounding of M (s equal to a steering vector).  Such cells
 // are re-scanned exactly in fp64 from the reference's fp64 steering table (rare, lane-divergent path).
+#include <cstdlib>
+
 #include "rsl_common.h"
 #include "rsl_internal.h"
 
@@ -29,15 +31,14 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr float kToepScale = 256.f;
 
-// B operand of one cell for this lane: entries e[16 kb + 8 h + j] of
-// [r0, Re r1, Im r1, ..., Re r_{M-1}, Im r_{M-1}, 0...] (normalised signature, x 2^8), split hi/lo.
+// The Toeplitz B column of one cell: e = [r0, Re r1, Im r1, ..., Re r_{M-1}, Im r_{M-1}, 0...] of the unit-norm
+// signature, scaled by 2^8 (exact), fp32.
 template <int MA, int KB>
-RSL_DEV void toep_operand(const float2 (&s)[MA], int h, half8 (&bhi)[KB], half8 (&blo)[KB]) {
+RSL_DEV void toep_entries(const float2 (&s)[MA], float (&e)[16 * KB]) {
   float pw = 0.f;
 #pragma unroll
   for (int m = 0; m < MA; ++m) pw = fmaf(s[m].x, s[m].x, fmaf(s[m].y, s[m].y, pw));
   const float inv = pw > 0.f ? kToepScale / pw : 0.f;  // angle_estimation.py:86-88 (unit-norm s)
-  float e[16 * KB];
   e[0] = pw > 0.f ? kToepScale : 0.f;
 #pragma unroll
   for (int k = 1; k < MA; ++k) {
@@ -52,16 +53,29 @@ RSL_DEV void toep_operand(const float2 (&s)[MA], int h, half8 (&bhi)[KB], half8 
   }
 #pragma unroll
   for (int x = 2 * MA - 1; x < 16 * KB; ++x) e[x] = 0.f;
+}
+
+// fp16 hi/lo split of 8 consecutive entries, packed two halves per dword (4 + 4 dwords).
+RSL_DEV void split8(const float* v, uint4& hi, uint4& lo) {
+  unsigned h[4], l[4];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = h ? e[16 * kb + 8 + j] : e[16 * kb + j];
-      const _Float16 hi = (_Float16)v;
-      bhi[kb][j] = hi;
-      blo[kb][j] = (_Float16)(v - (float)hi);
-    }
+  for (int j = 0; j < 4; ++j) {
+    const _Float16 h0 = (_Float16)v[2 * j], h1 = (_Float16)v[2 * j + 1];
+    const _Float16 l0 = (_Float16)(v[2 * j] - (float)h0), l1 = (_Float16)(v[2 * j + 1] - (float)h1);
+    h[j] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+    l[j] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
   }
+  hi = make_uint4(h[0], h[1], h[2], h[3]);
+  lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+RSL_DEV uint4 shfl_xor32_u4(uint4 v) {
+  return make_uint4((unsigned)__shfl_xor((int)v.x, 32), (unsigned)__shfl_xor((int)v.y, 32),
+                    (unsigned)__shfl_xor((int)v.z, 32), (unsigned)__shfl_xor((int)v.w, 32));
+}
+
+RSL_DEV uint4 sel_u4(bool c, uint4 a, uint4 b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
 template <int MA>
@@ -123,9 +137,12 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
   gval = (float)bp;
 }
 
-// One wave = 32 cells per pass (columns of a 32x32 MFMA tile; lanes l and l+32 share a cell and hold the two
-// K halves).  Grid tiles of 32 grid points are processed in pairs (two independent accumulator chains).
-template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS>
+// One wave = 64 cells per pass: lane (n, h) = (l & 31, l >> 5) loads, normalises and owns cell 64 ch + 32 h + n.
+// The two 32-cell halves are the two column tiles of v_mfma_f32_32x32x16_f16 (B: lane holds K rows 8h..8h+7 of
+// column n), so each lane computes the Toeplitz column of its own cell once and swaps the other K half with
+// lane l ^ 32 (no redundant loads or autocorrelations), and the fused ESPRIT / phase work of a pass is spread
+// over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0>
 __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
@@ -141,29 +158,34 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, n = lane & 31;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
-  const long long nch = (ncell + 31) >> 5;
+  const long long nch = (ncell + 63) >> 6;
   const long long stride = (long long)gridDim.x * 4;
   long long ch = (long long)blockIdx.x * 4 + wave;
   const float mthr = ((float)A - 1e-4f) * kToepScale;
   float2 ns[MA];
   if (ch < nch) {
-    const long long c = ch * 32 + n;
-    load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
+    const long long c = ch * 64 + lane;
+    if constexpr (DBG == 3) {
+#pragma unroll
+      for (int m = 0; m < MA; ++m) ns[m] = make_float2(0.1f * (lane + m), 0.2f * m - lane * 0.01f);
+    } else {
+      load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
+    }
   }
   for (; ch < nch; ch += stride) {
     float2 s[MA];
 #pragma unroll
     for (int m = 0; m < MA; ++m) s[m] = ns[m];
-    const long long c = ch * 32 + n;
+    const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
-    if (nx < nch) {  // prefetch the next chunk's signatures while this chunk's scan runs
-      const long long c2 = nx * 32 + n;
+    if (nx < nch && DBG != 3) {  // prefetch the next pass's signatures while this pass's scan runs
+      const long long c2 = nx * 64 + lane;
       load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns);
     }
     if constexpr (EXTRAS) {
-      // fused K6 (k_cell_extras), before the scan so its registers are dead during the MFMA loop: lanes h = 0
-      // write ESPRIT (angle_estimation.py:178-225), lanes h = 1 the spatial phase angle(s1 conj(s0))
-      // (velocity_solver.py:136).  fp32 closed form from the fp32 signature, fp64 asin.
+      // fused K6 (k_cell_extras) for the own cell, before the scan so its registers are dead during the MFMA
+      // loop: ESPRIT (angle_estimation.py:178-225) and the spatial phase angle(s1 conj(s0)) (velocity_solver.py
+      // :136); fp32 closed form from the fp32 signature, fp64 asin.
       float sr[MA], si[MA], pw = 0.f;
 #pragma unroll
       for (int m = 0; m < MA; ++m) {
@@ -179,90 +201,121 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
           si[m] *= sc;
         }
       }
-      float y, x;
-      bool zero = false;
-      if (h == 0) {
-        float nr, ni, dd;
-        esprit_phi<MA>(sr, si, A, nr, ni, dd);
-        y = ni;
-        x = nr;
-        zero = !(dd > 0.f);
-      } else {
-        y = si[1] * sr[0] - sr[1] * si[0];  // s1 * conj(s0)
-        x = sr[1] * sr[0] + si[1] * si[0];
-      }
-      const float ang = zero ? 0.f : atan2f(y, x);
       if (c < ncell) {
-        if (h == 0) {
-          if (out_esprit) out_esprit[c] = asin((double)ang * esprit_scale) * (180.0 / 3.14159265358979323846);
-        } else if (out_phase) {
-          out_phase[c] = (double)ang;
+        if (out_esprit) {
+          float nr, ni, dd;
+          esprit_phi<MA>(sr, si, A, nr, ni, dd);
+          const float ang = dd > 0.f ? atan2f(ni, nr) : 0.f;
+          out_esprit[c] = asin((double)ang * esprit_scale) * (180.0 / 3.14159265358979323846);
         }
+        if (out_phase) out_phase[c] = (double)atan2f(si[1] * sr[0] - sr[1] * si[0], sr[1] * sr[0] + si[1] * si[0]);
       }
     }
-    half8 bhi[KB], blo[KB];
-    toep_operand<MA, KB>(s, h, bhi, blo);
-    // Argmax epilogue.  Per tile: the tile max (8 v_max3), a strict '>' record test against the running best,
-    // and a conditional copy of the record tile's 16 values; the in-tile index is resolved once per chunk.
-    // Tiles ascend in g and in-tile values ascend in row ((i&3) + 8(i>>2) + 4h), so the first index wins as
-    // in np.argmax.  Rows past G replicate row G-1 and so never win.
-    float best = -INFINITY;
-    int bt = 0;
-    float sv[16];
+    // B operands of the two column tiles: own K half from the own cell, the other half from lane ^ 32
+    uint4 b0h[KB], b0l[KB], b1h[KB], b1l[KB];
+    {
+      float e[16 * KB];
+      if constexpr (DBG == 4) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sv[i] = 0.f;
-    for (int t = 0; t < ntiles; t += 2) {
+        for (int x = 0; x < 16 * KB; ++x) e[x] = s[x % MA].x;
+      } else {
+        toep_entries<MA, KB>(s, e);
+      }
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        uint4 oh, ol, xh, xl;
+        split8(e + 16 * kb + 8 * h, oh, ol);        // own cell, K rows 8h..8h+7
+        split8(e + 16 * kb + 8 * (1 - h), xh, xl);  // own cell, the partner's K half
+        const uint4 rh = shfl_xor32_u4(xh), rl = shfl_xor32_u4(xl);  // partner's cell, K rows 8h..8h+7
+        b0h[kb] = sel_u4(h == 0, oh, rh);
+        b0l[kb] = sel_u4(h == 0, ol, rl);
+        b1h[kb] = sel_u4(h == 0, rh, oh);
+        b1l[kb] = sel_u4(h == 0, rl, ol);
+      }
+    }
+    // Argmax epilogue per column tile: the tile max (v_max3 tree), a strict '>' record test and a conditional
+    // copy of the record tile's 16 values; the in-tile index is resolved once per pass.  Tiles ascend in g and
+    // in-tile values ascend in row ((i&3) + 8(i>>2) + 4h): the first index wins as in np.argmax.  Rows past G
+    // replicate row G-1 and so never win.
+    float best0 = -INFINITY, best1 = -INFINITY;
+    int bt0 = 0, bt1 = 0;
+    float sv0[16], sv1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sv0[i] = 0.f;
+      sv1[i] = 0.f;
+    }
+    for (int t = 0; t < ntiles; ++t) {
       floatx16 acc0 = {}, acc1 = {};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const uint4 h0 = tt[(((t * KB + kb) * 2) + 0) * 64 + lane];
-        const uint4 l0 = tt[(((t * KB + kb) * 2) + 1) * 64 + lane];
-        const uint4 h1 = tt[((((t + 1) * KB + kb) * 2) + 0) * 64 + lane];
-        const uint4 l1 = tt[((((t + 1) * KB + kb) * 2) + 1) * 64 + lane];
-        const half8 ah0 = __builtin_bit_cast(half8, h0), al0 = __builtin_bit_cast(half8, l0);
-        const half8 ah1 = __builtin_bit_cast(half8, h1), al1 = __builtin_bit_cast(half8, l1);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al0, bhi[kb], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al1, bhi[kb], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, blo[kb], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, blo[kb], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah0, bhi[kb], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah1, bhi[kb], acc1, 0, 0, 0);
+        const half8 ah = __builtin_bit_cast(half8, tt[(((t * KB + kb) * 2) + 0) * 64 + lane]);
+        const half8 al = __builtin_bit_cast(half8, tt[(((t * KB + kb) * 2) + 1) * 64 + lane]);
+        const half8 x0h = __builtin_bit_cast(half8, b0h[kb]), x0l = __builtin_bit_cast(half8, b0l[kb]);
+        const half8 x1h = __builtin_bit_cast(half8, b1h[kb]), x1l = __builtin_bit_cast(half8, b1l[kb]);
+        if constexpr (DBG == 2) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            acc0[i] += (float)ah[i & 7] * (float)x0h[(i + 1) & 7];
+            acc1[i] += (float)al[i & 7] * (float)x1l[(i + 3) & 7];
+          }
+        } else {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, x0h, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, x1h, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x0l, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x1l, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x0h, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x1h, acc1, 0, 0, 0);
+        }
       }
       {
         const float m = tile_max(acc0);
-        const bool u = m > best;
-        best = u ? m : best;
-        bt = u ? t : bt;
+        const bool u = m > best0;
+        best0 = u ? m : best0;
+        bt0 = u ? t : bt0;
+        if constexpr (DBG != 1) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sv[i] = u ? acc0[i] : sv[i];
+          for (int i = 0; i < 16; ++i) sv0[i] = u ? acc0[i] : sv0[i];
+        }
       }
       {
         const float m = tile_max(acc1);
-        const bool u = m > best;
-        best = u ? m : best;
-        bt = u ? t + 1 : bt;
+        const bool u = m > best1;
+        best1 = u ? m : best1;
+        bt1 = u ? t : bt1;
+        if constexpr (DBG != 1) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sv[i] = u ? acc1[i] : sv[i];
+          for (int i = 0; i < 16; ++i) sv1[i] = u ? acc1[i] : sv1[i];
+        }
       }
     }
-    int ii = 15;
+    int i0 = 15, i1 = 15;
 #pragma unroll
-    for (int i = 14; i >= 0; --i) ii = (sv[i] == best) ? i : ii;
-    int bidx = 32 * bt + 4 * h + (ii & 3) + 8 * (ii >> 2);
-    // merge the two K-half lanes of each cell (first index wins on ties)
-    {
-      const float ob = __shfl_xor(best, 32);
-      const int oi = __shfl_xor(bidx, 32);
-      const bool take = (ob > best) | ((ob == best) & (oi < bidx));
-      best = take ? ob : best;
-      bidx = take ? oi : bidx;
+    for (int i = 14; i >= 0; --i) {
+      i0 = (sv0[i] == best0) ? i : i0;
+      i1 = (sv1[i] == best1) ? i : i1;
     }
+    int g0 = 32 * bt0 + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
+    int g1 = 32 * bt1 + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
+    // merge the two K-half lanes of each column (first index wins on ties)
+    {
+      const float ob0 = __shfl_xor(best0, 32), ob1 = __shfl_xor(best1, 32);
+      const int og0 = __shfl_xor(g0, 32), og1 = __shfl_xor(g1, 32);
+      const bool tk0 = (ob0 > best0) | ((ob0 == best0) & (og0 < g0));
+      const bool tk1 = (ob1 > best1) | ((ob1 == best1) & (og1 < g1));
+      best0 = tk0 ? ob0 : best0;
+      g0 = tk0 ? og0 : g0;
+      best1 = tk1 ? ob1 : best1;
+      g1 = tk1 ? og1 : g1;
+    }
+    float best = h ? best1 : best0;  // own cell = column tile h
+    int bidx = h ? g1 : g0;
     if (bidx >= G) bidx = G - 1;
     float gval = best * (1.0f / kToepScale);
     if constexpr (MUSIC) {
-      if (best >= mthr && h == 0 && c < ncell) exact_scan<MA>(s, A, G, steer64, bidx, gval);  // rare
+      if (best >= mthr && c < ncell) exact_scan<MA>(s, A, G, steer64, bidx, gval);  // rare
     }
-    if (h == 0 && c < ncell) {
+    if (c < ncell) {
       out_idx[c] = bidx;
       if constexpr (GMAX) out_gmax[c] = gval;
     }
@@ -275,6 +328,15 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
                                 int ntiles, int G, const double* steer64, int* out_idx, float* out_gmax,
                                 double esprit_scale, double* out_esprit, double* out_phase, int max_blocks) {
   auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS>;
+  if constexpr (MUSIC && !GMAX && !EXTRAS && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing studies only)
+    if (const char* e = getenv("RSL_DOA_DBG")) {
+      const int v = atoi(e);
+      if (v == 1) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 1>;
+      if (v == 2) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 2>;
+      if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3>;
+      if (v == 4) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 4>;
+    }
+  }
   const size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);
   if (lds > 64 * 1024) return hipErrorInvalidValue;  // caller checks toep_table_fits()
   int nb = 0;
@@ -297,7 +359,7 @@ hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int 
   if (A < 1 || A > 16 || (ntiles32 & 1)) return hipErrorInvalidValue;
   if (music && !steer64) return hipErrorInvalidValue;
   if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
-  const long long max_blocks = ncell_dev ? 0 : (ncell_host + 127) / 128;
+  const long long max_blocks = ncell_dev ? 0 : (ncell_host + 255) / 256;  // 4 waves x 64 cells
   if (!ncell_dev && ncell_host <= 0) return hipSuccess;
   const uint4* tab = reinterpret_cast<const uint4*>(toep_tab);
   const bool gm = out_gmax != nullptr, ex = out_esprit || out_phase;

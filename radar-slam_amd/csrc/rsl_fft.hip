@@ -227,8 +227,8 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-template <int C, int KB>
-__global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __restrict__ work, int S,
+template <int C, int KB, int NT>
+__global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
                                                              float thr_f, int i_lo, int i_hi,
                                                              unsigned long long* __restrict__ mask,
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
   constexpr int NR = KB + 2;
   constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
   constexpr int W = (C + 63) / 64;
-  constexpr int PER = (NR * C + kThreads - 1) / kThreads;
+  constexpr int PER = (NR * C + NT - 1) / NT;
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + C;
@@ -246,9 +246,9 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
   const int kb = blockIdx.x % nkb;
   const long fa = blockIdx.x / nkb;
   const int k0 = kb * KB;
-  for (int k = tid; k < C; k += kThreads) tws[k] = tw[k];
+  for (int k = tid; k < C; k += NT) tws[k] = tw[k];
   const float2* src = work + (size_t)fa * C * S;
-  for (int idx = tid; idx < C * NR; idx += kThreads) {
+  for (int idx = tid; idx < C * NR; idx += NT) {
     const int c = idx / NR, r = idx - c * NR;
     int k = k0 - 1 + r;  // unshifted range bin of LDS row r
     if (k < 0) k += S;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
     buf[r * LD + lp(c)] = src[(size_t)c * S + k];
   }
   __syncthreads();
-  fft_rows<C, NR, kThreads, LD>(buf, tws, tid);
+  fft_rows<C, NR, NT, LD>(buf, tws, tid);
   const int hs = S / 2, hc = C / 2;
   int i0 = k0 + hs;  // shifted row of LDS row 1
   if (i0 >= S) i0 -= S;
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
   float pr[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * kThreads;
+    const int idx = tid + q * NT;
     pr[q] = 0.f;
     if (idx < NR * C) {
       const int r = idx / C, j = idx - r * C;  // j: shifted doppler index
@@ -280,12 +280,12 @@ __global__ __launch_bounds__(kThreads) void k_doppler_detect(const float2* __res
   float* pw = reinterpret_cast<float*>(buf);  // power tile [NR][C], shifted doppler order
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * kThreads;
+    const int idx = tid + q * NT;
     if (idx < NR * C) pw[idx] = pr[q];
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  for (int kk = wave; kk < KB; kk += kThreads / 64) {
+  for (int kk = wave; kk < KB; kk += NT / 64) {
     const int i = i0 + kk;
     const bool gate = (i >= i_lo && i <= i_hi);
     const bool has_up = i > 0, has_dn = i + 1 < S;
@@ -327,7 +327,10 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
   // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
-  hipLaunchKernelGGL((k_doppler_detect<C, KB>), dim3((unsigned)ntile), dim3(kThreads), lds, st, work, S, tw, rds,
+  // 256 threads (a 320-thread block that runs each radix-8 stage of the 18-row KB-16 tile in one pass measured
+  // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_doppler_detect<C, KB, NT>), dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds,
                      thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
   return hipGetLastError();
 }
