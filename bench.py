@@ -28,6 +28,21 @@ sys.path.insert(0, os.path.join(ROOT, 'radar-slam_amd'))
 METRIC = "radar frames/sec end-to-end, 8ch×128chirp×512 cube; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
+PROFILE = os.path.join(ROOT, 'profiles', 'r1_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+
+
+def pmc_traffic(kernel_prefix, frames_per_launch):
+    """HBM bytes per launch of a kernel from the committed PMC profile (FETCH_SIZE x 2 + WRITE_SIZE, per
+    MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present."""
+    try:
+        prof = json.load(open(PROFILE))
+    except (OSError, ValueError):
+        return None
+    for name, e in prof.get('kernels', {}).items():
+        if name.startswith('rsl::' + kernel_prefix) and 'hbm_bytes' in e:
+            return e['hbm_bytes'] * frames_per_launch / prof.get('frames_per_launch', 1000)
+    return None
 SCENE = [  # tests/test_synth_raw.py:165-190 (reference)
     (20.0, 0.0, -10.0, 0.0), (40.0, math.radians(45.0), -8.0, 5.0), (60.0, math.radians(-30.0), -12.0, -3.0)]
 
@@ -123,6 +138,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--no-timing', action='store_true', help='disable per-kernel hipEvent timing')
+    ap.add_argument('--streams', type=int, default=int(os.environ.get('RSL_BENCH_STREAMS', '1')),
+                    help='concurrent HIP streams per GPU; each runs the chain on F/streams frames of the step')
     args = ap.parse_args()
 
     import torch
@@ -140,23 +157,38 @@ def main():
     A, C, S, F = 8, 128, 512, args.frames_per_step
     cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=51.2e-6)
     ctx = rsl.get_context(local)
-    chain = rsl.RadarChain(cfg, F, ctx)
+    NS = max(1, args.streams)
+    if F % NS:
+        raise SystemExit('--frames-per-step must be a multiple of --streams')
+    vel = torch.empty((F, 8), dtype=torch.float64, device=dev)
+    chains = [rsl.RadarChain(cfg, F // NS, ctx, vel_out=vel[k * (F // NS):(k + 1) * (F // NS)]) for k in range(NS)]
+    chain = chains[0]
+    streams = [torch.cuda.Stream(dev) for _ in range(NS)]
     nb = 2
     cubes = make_cubes(torch, dev, nb, F, A, C, S, seed=1234 + 7919 * rank)
     # trajectory reduction: device prefix scan of this rank's frame block, all-gather of the
     # 16-double block summaries and of the per-frame poses over RCCL/xGMI (rsl/traj.py)
     reducer = rsl.TrajectoryReducer(ctx, F, dt=cfg.dt)
 
+    main = torch.cuda.current_stream(dev)
+
     def step(i):
-        chain.run(cubes[i % nb])
-        reducer.step(chain.vel, vstride=chain.vel.shape[1], nv=2)
+        cube = cubes[i % nb]
+        for k, (ch, st) in enumerate(zip(chains, streams)):  # independent frame slices, concurrent streams
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                ch.run(cube[k * (F // NS):(k + 1) * (F // NS)])
+        for st in streams:
+            main.wait_stream(st)
+        reducer.step(vel, vstride=vel.shape[1], nv=2)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    ne, nc = chain.totals()
-    if ne > chain.entry_cap or nc > chain.cell_cap:
-        raise RuntimeError('peak capacity exceeded')
+    for ch in chains:
+        ne, nc = ch.totals()
+        if ne > ch.entry_cap or nc > ch.cell_cap:
+            raise RuntimeError('peak capacity exceeded')
     if not args.no_timing:
         ctx.timing(True)
         ctx.timing_reset()
@@ -177,7 +209,8 @@ def main():
         elapsed = float(tt.item())
     kt = ctx.timing_read() if not args.no_timing else {}
     ctx.timing(False)
-    ne, nc = chain.totals()
+    ne = sum(ch.totals()[0] for ch in chains)
+    nc = sum(ch.totals()[1] for ch in chains)
     frames_total = F * args.steps * world
     fps = frames_total / elapsed
 
@@ -191,26 +224,34 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "configs[2]: 8ch x 128chirp x 512 synthetic cube, full chain "
-                               "(RDS + peaks + MUSIC argmax + ESPRIT + LS velocity)",
+                               "(RDS + peaks + MUSIC argmax + ESPRIT + LS velocity + trajectory)",
                    "frames_per_step": F, "frames_per_gpu_per_step": F, "antennas": A, "chirps": C, "samples": S,
-                   "doa_grid": G, "parallelism": f"frame-sharded x{world}"},
+                   "doa_grid": G, "streams_per_gpu": NS, "parallelism": f"frame-sharded x{world}"},
         "peaks_per_frame": ne / F, "cells_per_frame": nc / F,
     }
     if kt:
-        ms_doa, n_doa = kt['doa_scan']
-        flops = nc * G * (8 * A + 5)               # per launch: unique cells x grid x (8M + 5)
-        t_doa = ms_doa / max(n_doa, 1) * 1e-3
+        # per-launch figures: each kernel runs once per stream per step on F / NS frames
+        per = lambda name: kt[name][0] / max(kt[name][1], 1)  # ms per launch
+        Fl = F // NS
+        ncl = nc / NS                                          # unique cells per launch
+        # Dominant kernel: the fused DoA scan (k_doa_toep).  Algorithmic work of its formulation: one real dot
+        # product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2), evaluated as three f16
+        # MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops; bound: dense f16 MFMA peak.
+        t_doa = per('doa_scan') * 1e-3
+        flops = 3 * 2 * (2 * A - 1) * ncl * G
         ach = flops / t_doa / 1e12
-        line["roofline"] = {"bound": "mfma", "kernel": "k_doa_scan", "achieved": ach, "peak": FP32_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": ach / FP32_PEAK_TFLOPS, "traffic": None,
-                            "avg_launch_ms": ms_doa / max(n_doa, 1),
-                            "algorithmic_flops_per_launch": flops}
-        t_fft = (kt['range_fft'][0] + kt['doppler_fft'][0]) / max(kt['range_fft'][1], 1) * 1e-3
-        fft_bytes = 2 * A * C * S * 8 * F
-        line["fft_stage"] = {"bound": "hbm", "achieved": fft_bytes / t_fft / 1e9, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": fft_bytes / t_fft / 1e9 / HBM_PEAK_GBS,
-                             "algorithmic_bytes_per_launch": fft_bytes}
-        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) for k, v in kt.items() if v[1]}
+        line["roofline"] = {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                            "traffic": pmc_traffic('k_doa_toep', Fl), "avg_launch_ms": per('doa_scan'),
+                            "algorithmic_flops_per_launch": flops,
+                            "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
+        # FFT stage (K1 + K2/K3): HBM-bound; algorithmic bytes = read the c64 cube + write the c64 RDS
+        t_fft = (per('range_fft') + per('doppler_fft')) * 1e-3
+        fft_bytes = 2 * A * C * S * 8 * Fl
+        line["fft_stage"] = {"bound": "hbm", "kernels": ["k_range_fft_p", "k_doppler_detect"],
+                             "achieved": fft_bytes / t_fft / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": fft_bytes / t_fft / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fft_bytes}
+        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
     if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)

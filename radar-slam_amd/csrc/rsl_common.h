@@ -160,6 +160,14 @@ struct Dft {
 // LDS position of FFT point x in a padded row: one pad slot after every 8 points.  Radix-8 Stockham writes
 // (stride 8 points = 64 B per lane) and the 8-lane-group pattern of the second stage then land on distinct
 // banks; unpadded they are 4- to 8-way bank conflicts.
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (observed placement, speed only), so
+// logical tile L = (b % 8) * (n / 8) + b / 8 gives each XCD a contiguous run of tiles, dispatched back to back:
+// tiles sharing halo cache lines then meet in the same 4 MiB L2.  The n % 8 tail keeps the identity order.
+RSL_DEV long xcd_tile(long b, long n) {
+  const long n8 = n & ~7L;
+  return b < n8 ? (b & 7) * (n8 >> 3) + (b >> 3) : b;
+}
+
 RSL_DEV constexpr int lp(int x) { return x + (x >> 3); }
 // Padded row length for N points.
 constexpr int lp_row(int N) { return N + (N + 7) / 8; }

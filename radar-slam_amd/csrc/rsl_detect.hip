@@ -220,7 +220,9 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
 // (consecutive lanes -> consecutive addresses); scattered 4-byte stores from a per-word set-bit loop would cost
 // one memory request per lane.  Entries follow dechirp.py:257 (np.where order: antenna -> range -> doppler);
 // cells are range-major unions over antennas.  power_db comes from the row-compact peak powers of k_detect
-// (no RDS re-read), 10 log10 in fp32 (the powers are fp32), stored as float64 like power_spectrum_db.  A block with more than kEmitCap items falls back to the per-word loop.
+// (no RDS re-read), 10 log10 in fp32 (the powers are fp32), stored as float64 like power_spectrum_db.  A block with more than kEmitCap items
+// runs phases 1-2 in rounds of kEmitCap (a per-word store loop would scatter 4-byte stores: measured 2.9x HBM write
+// amplification on the 54%-dense cell unions of cfg2).
 constexpr int kEmitCap = 4096;
 
 RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
@@ -310,83 +312,62 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
 #pragma unroll
     for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
   }
-  if (total > kEmitCap) {  // rare: dense block, per-word loop with scattered stores
-    __syncthreads();
-    long long k = s_first + loc;
-    int r = r0;
-    while (m) {
-      const int b = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      if (entries) {
-        if (k < entry_cap) {
-          e_ant[k] = a;
-          e_rbin[k] = i;
-          e_dbin[k] = w * 64 + b;
-          e_cell[k] = cw + __popcll(u & ((1ull << b) - 1ull));
-          if (e_pdb) e_pdb[k] = (double)(10.0f * log10f(pk_pow[(size_t)row * C + r] + 1e-12f));
-        }
-      } else if (k < cell_cap) {
-        unsigned am = 0;
-#pragma unroll
-        for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
-        c_frame[k] = (int)f;
-        c_rc[k] = i * C + w * 64 + b;
-        c_amask[k] = am;
-      }
-      ++r;
-      ++k;
-    }
-    return;
-  }
-  // phase 1: packed (word, bit) codes (+ the cell's antenna mask) and per-word side data in LDS
-  {
-    unsigned long long mm = m;
-    int o = loc;
-    while (mm) {
-      const int b = __ffsll((long long)mm) - 1;
-      mm &= mm - 1;
-      pk[o] = ((unsigned)t << 6) | (unsigned)b;
-      if (!entries) {
-        unsigned am = 0;
-#pragma unroll
-        for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
-        pam[o] = am;
-      }
-      ++o;
-    }
-  }
   s_loc[t] = loc;
   s_r0[t] = r0;
   s_cw[t] = cw;
   s_u[t] = u;
   s_fi[t] = entries ? ((a << 16) | i) : (int)f;
-  __syncthreads();
-  const long long first = s_first;
   const long long gw0 = gw - t;  // first word of the block
-  // phase 2: coalesced stores, lane k % 256 writes item k (no divisions: per-word data come from LDS)
-  for (int k = t; k < total; k += 256) {
-    const unsigned code = pk[k];
-    const int tt = (int)(code >> 6), b = (int)(code & 63);
-    const long long g2 = gw0 + tt;
-    const int ww = (int)(g2 % W);
-    const long long e = first + k;
-    if (entries) {
-      if (e < entry_cap) {
-        const int ai = s_fi[tt];
-        const int ii = ai & 0xffff;
-        const int r = s_r0[tt] + (k - s_loc[tt]);
-        e_ant[e] = ai >> 16;
-        e_rbin[e] = ii;
-        e_dbin[e] = ww * 64 + b;
-        e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
-        if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)(g2 / W) * C + r] + 1e-12f));  // dechirp.py:235-236
+  // rounds of kEmitCap items (one round unless the block is dense, e.g. the cell union at high peak density)
+  for (int base = 0; base < total; base += kEmitCap) {
+    // phase 1: packed (word, bit) codes (+ the cell's antenna mask) of this round's items, in LDS
+    if (loc < base + kEmitCap && loc + cnt > base) {
+      unsigned long long mm = m;
+      int o = loc;
+      while (mm && o < base + kEmitCap) {
+        const int b = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        if (o >= base) {
+          pk[o - base] = ((unsigned)t << 6) | (unsigned)b;
+          if (!entries) {
+            unsigned am = 0;
+#pragma unroll
+            for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
+            pam[o - base] = am;
+          }
+        }
+        ++o;
       }
-    } else if (e < cell_cap) {
-      const long long rw = g2 / W;
-      c_frame[e] = s_fi[tt];
-      c_rc[e] = (int)(rw - (long long)s_fi[tt] * S) * C + ww * 64 + b;
-      c_amask[e] = pam[k];
     }
+    __syncthreads();
+    const long long first = s_first + base;
+    const int nk = total - base < kEmitCap ? total - base : kEmitCap;
+    // phase 2: coalesced stores, lane k % 256 writes item k (no divisions: per-word data come from LDS)
+    for (int k = t; k < nk; k += 256) {
+      const unsigned code = pk[k];
+      const int tt = (int)(code >> 6), b = (int)(code & 63);
+      const long long g2 = gw0 + tt;
+      const int ww = (int)(g2 % W);
+      const long long e = first + k;
+      if (entries) {
+        if (e < entry_cap) {
+          const int ai = s_fi[tt];
+          const int ii = ai & 0xffff;
+          const int r = s_r0[tt] + (base + k - s_loc[tt]);
+          e_ant[e] = ai >> 16;
+          e_rbin[e] = ii;
+          e_dbin[e] = ww * 64 + b;
+          e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
+          if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)(g2 / W) * C + r] + 1e-12f));  // dechirp.py:235-236
+        }
+      } else if (e < cell_cap) {
+        const long long rw = g2 / W;
+        c_frame[e] = s_fi[tt];
+        c_rc[e] = (int)(rw - (long long)s_fi[tt] * S) * C + ww * 64 + b;
+        c_amask[e] = pam[k];
+      }
+    }
+    __syncthreads();  // pk / pam reused by the next round
   }
 }
 

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
                                                              float thr_f, int i_lo, int i_hi,
                                                              unsigned long long* __restrict__ mask,
                                                              int* __restrict__ row_count, float* __restrict__ dbmap,
-                                                             float* __restrict__ pk_pow) {
+                                                             float* __restrict__ pk_pow, int xcd) {
   constexpr int NR = KB + 2;
   constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
   constexpr int W = (C + 63) / 64;
@@ -243,8 +243,9 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   float2* buf = sm + C;
   const int tid = threadIdx.x;
   const int nkb = S / KB;
-  const int kb = blockIdx.x % nkb;
-  const long fa = blockIdx.x / nkb;
+  const long tile = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (long)blockIdx.x;
+  const int kb = (int)(tile % nkb);
+  const long fa = tile / nkb;
   const int k0 = kb * KB;
   for (int k = tid; k < C; k += NT) tws[k] = tw[k];
   const float2* src = work + (size_t)fa * C * S;
@@ -318,6 +319,12 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   }
 }
 
+// XCD-grouped tile order (default on; RSL_DD_XCD=0 for the dispatch order, A/B tuning)
+static int dd_xcd() {
+  const char* e = getenv("RSL_DD_XCD");
+  return e ? atoi(e) != 0 : 1;
+}
+
 template <int C, int KB>
 static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw,
                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
@@ -331,7 +338,7 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
   constexpr int NT = 256;
   hipLaunchKernelGGL((k_doppler_detect<C, KB, NT>), dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds,
-                     thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+                     thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow, dd_xcd());
   return hipGetLastError();
 }
 

@@ -57,7 +57,9 @@ class ChainConfig:
 
 
 class RadarChain:
-    def __init__(self, cfg: ChainConfig, frames: int, ctx: Optional[Context] = None):
+    def __init__(self, cfg: ChainConfig, frames: int, ctx: Optional[Context] = None, vel_out=None):
+        """vel_out: optional device f64 [frames, 8] view receiving the per-frame velocity rows (lets several
+        chains on different streams fill consecutive slices of one buffer)."""
         self.cfg, self.F = cfg, int(frames)
         self.ctx = ctx or get_context()
         torch, ctx = self.ctx.torch, self.ctx
@@ -94,7 +96,7 @@ class RadarChain:
                           c_frame=e((cc,), torch.int32), c_rc=e((cc,), torch.int32), c_amask=e((cc,), torch.int32))
         self.gidx = e((cc,), torch.int32)
         self.ext = dict(esprit=e((cc,), torch.float64), phase=e((cc,), torch.float64), az=e((cc,), torch.float64))
-        self.vel = e((F, 8), torch.float64)
+        self.vel = vel_out if vel_out is not None else e((F, 8), torch.float64)
         self.ncell_dev = self.offs['cell_base'][F:F + 1]
         # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
         self.fused_doa = bool(self.steer['toeplitz']) and A >= 2

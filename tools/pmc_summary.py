@@ -48,8 +48,9 @@ def main():
     ap.add_argument('--extra', nargs='*', default=[])
     ap.add_argument('--out', required=True)
     ap.add_argument('--note', default='')
+    ap.add_argument('--frames-per-launch', type=int, default=1000)
     a = ap.parse_args()
-    res = {'note': a.note, 'kernels': {}}
+    res = {'note': a.note, 'frames_per_launch': a.frames_per_launch, 'kernels': {}}
     st = stats(a.stats) if a.stats else {}
     fe = counters(a.fetch) if a.fetch else {}
     wr = counters(a.write) if a.write else {}
