@@ -247,14 +247,35 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   const int kb = (int)(tile % nkb);
   const long fa = tile / nkb;
   const int k0 = kb * KB;
-  for (int k = tid; k < C; k += NT) tws[k] = tw[k];
   const float2* src = work + (size_t)fa * C * S;
-  for (int idx = tid; idx < C * NR; idx += NT) {
-    const int c = idx / NR, r = idx - c * NR;
-    int k = k0 - 1 + r;  // unshifted range bin of LDS row r
-    if (k < 0) k += S;
-    if (k >= S) k -= S;
-    buf[r * LD + lp(c)] = src[(size_t)c * S + k];
+  // all of the thread's loads in flight before the first LDS write (a rolled loop waits on each load in turn);
+  // the twiddles first, so their LDS copy waits only on them
+  constexpr int TWP = (C + NT - 1) / NT;
+  float2 twv[TWP];
+#pragma unroll
+  for (int q = 0; q < TWP; ++q)
+    if (C % NT == 0 || tid + q * NT < C) twv[q] = tw[tid + q * NT];
+  float2 ld[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    if ((NR * C) % NT == 0 || idx < NR * C) {
+      const int c = idx / NR, r = idx - c * NR;
+      int k = k0 - 1 + r;  // unshifted range bin of LDS row r
+      k = k < 0 ? k + S : (k >= S ? k - S : k);
+      ld[q] = src[(unsigned)(c * S + k)];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < TWP; ++q)
+    if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    if ((NR * C) % NT == 0 || idx < NR * C) {
+      const int c = idx / NR, r = idx - c * NR;
+      buf[r * LD + lp(c)] = ld[q];
+    }
   }
   __syncthreads();
   fft_rows<C, NR, NT, LD>(buf, tws, tid);
