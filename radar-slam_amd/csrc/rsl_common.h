@@ -187,8 +187,14 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
     if ((TOT % NT) == 0 || idx < TOT) {
       const int row = idx / NB, j = idx - (idx / NB) * NB;
       const float2* src = buf + row * LD;
+      if constexpr (NB % 8 == 0) {  // lp(j + r NB) = lp(j) + r (NB + NB/8): immediate LDS offsets
+        const float2* s0 = src + lp(j);
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[q][r] = src[lp(j + r * NB)];
+        for (int r = 0; r < R; ++r) v[q][r] = s0[r * (NB + NB / 8)];
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[q][r] = src[lp(j + r * NB)];
+      }
     }
   }
   __syncthreads();
@@ -206,8 +212,19 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
       Dft<R>::run(v[q]);
       float2* dst = buf + row * LD;
       const int o = (j / NS) * NS * R + k;
+      if constexpr (NS == 1 && R <= 8 && (R & (R - 1)) == 0) {
+        // o = j R: the R outputs never cross a pad slot, lp(o + r) = lp(o) + r
+        float2* d0 = dst + lp(o);
 #pragma unroll
-      for (int r = 0; r < R; ++r) dst[lp(o + r * NS)] = v[q][r];
+        for (int r = 0; r < R; ++r) d0[r] = v[q][r];
+      } else if constexpr (NS % 8 == 0) {
+        float2* d0 = dst + lp(o);
+#pragma unroll
+        for (int r = 0; r < R; ++r) d0[r * (NS + NS / 8)] = v[q][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[lp(o + r * NS)] = v[q][r];
+      }
     }
   }
   __syncthreads();

@@ -242,10 +242,10 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   float2* tws = sm;
   float2* buf = sm + C;
   const int tid = threadIdx.x;
-  const int nkb = S / KB;
-  const long tile = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (long)blockIdx.x;
+  const unsigned nkb = (unsigned)(S / KB);
+  const unsigned tile = xcd ? (unsigned)xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   const int kb = (int)(tile % nkb);
-  const long fa = tile / nkb;
+  const unsigned fa = tile / nkb;
   const int k0 = kb * KB;
   const float2* src = work + (size_t)fa * C * S;
   // all of the thread's loads in flight before the first LDS write (a rolled loop waits on each load in turn);
@@ -255,26 +255,64 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 #pragma unroll
   for (int q = 0; q < TWP; ++q)
     if (C % NT == 0 || tid + q * NT < C) twv[q] = tw[tid + q * NT];
-  float2 ld[PER];
+  // structured map: thread = (interior range bin ri, chirp slot cs), chirps cs + CS q at a constant stride
+  // (one address add per load, 128-B aligned row segments), then the two halo rows spread over all threads
+  constexpr int CS = NT / KB;
+  constexpr bool STRUCT = (NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16);
+  if constexpr (STRUCT) {
+    constexpr int PI = C / CS, PH = (2 * C + NT - 1) / NT;
+    const int ri = tid % KB, cs = tid / KB;
+    float2 ld[PI + PH];
+    const float2* p = src + (unsigned)(cs * S + k0 + ri);
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * NT;
-    if ((NR * C) % NT == 0 || idx < NR * C) {
-      const int c = idx / NR, r = idx - c * NR;
-      int k = k0 - 1 + r;  // unshifted range bin of LDS row r
-      k = k < 0 ? k + S : (k >= S ? k - S : k);
-      ld[q] = src[(unsigned)(c * S + k)];
+    for (int q = 0; q < PI; ++q) ld[q] = p[(unsigned)(q * CS * S)];
+    int kl = k0 - 1, kh = k0 + KB;  // halo range bins (periodic: reflect is applied in the detect stage)
+    if (kl < 0) kl += S;
+    if (kh >= S) kh -= S;
+#pragma unroll
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        ld[PI + h] = src[(unsigned)(c * S + (side ? kh : kl))];
+      }
     }
-  }
 #pragma unroll
-  for (int q = 0; q < TWP; ++q)
-    if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+    for (int q = 0; q < TWP; ++q)
+      if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+    float2* row = buf + (ri + 1) * LD + lp(cs);
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * NT;
-    if ((NR * C) % NT == 0 || idx < NR * C) {
-      const int c = idx / NR, r = idx - c * NR;
-      buf[r * LD + lp(c)] = ld[q];
+    for (int q = 0; q < PI; ++q) row[q * CS + ((q * CS) >> 3)] = ld[q];
+#pragma unroll
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        buf[(side ? NR - 1 : 0) * LD + lp(c)] = ld[PI + h];
+      }
+    }
+  } else {
+    float2 ld[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = tid + q * NT;
+      if ((NR * C) % NT == 0 || idx < NR * C) {
+        const int c = idx / NR, r = idx - c * NR;
+        int k = k0 - 1 + r;  // unshifted range bin of LDS row r
+        k = k < 0 ? k + S : (k >= S ? k - S : k);
+        ld[q] = src[(unsigned)(c * S + k)];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TWP; ++q)
+      if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int idx = tid + q * NT;
+      if ((NR * C) % NT == 0 || idx < NR * C) {
+        const int c = idx / NR, r = idx - c * NR;
+        buf[r * LD + lp(c)] = ld[q];
+      }
     }
   }
   __syncthreads();
