@@ -46,6 +46,28 @@ __device__ double qcost(double vx, double vy, double k, double ridge, const doub
          ridge * (vx * vx + vy * vy);
 }
 
+constexpr int kVelU = 8;
+
+// kVelU cells i0 + u * blockDim.x (u < kVelU) of one thread; cells at or past e read as weight 0, grid index 0
+RSL_DEV void vel_load(long long i0, long long e, const int* __restrict__ gidx, const double* __restrict__ y,
+                      const unsigned* __restrict__ amask, int (&gv)[kVelU], double (&yv)[kVelU],
+                      unsigned (&mv)[kVelU]) {
+#pragma unroll
+  for (int u = 0; u < kVelU; ++u) {
+    const long long i = i0 + (long long)u * blockDim.x;
+    const bool ok = i < e;
+    const long long ii = ok ? i : i0;  // i0 < e: always a valid address
+    gv[u] = gidx[ii];
+    yv[u] = y[ii];
+    mv[u] = amask ? amask[ii] : 1u;
+    if (!ok) {
+      gv[u] = 0;
+      yv[u] = 0.0;
+      mv[u] = 0u;
+    }
+  }
+}
+
 __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az, const int* __restrict__ gidx,
                                                   const double* __restrict__ az_table, int G,
                                                   const double* __restrict__ y, const unsigned* __restrict__ amask,
@@ -65,17 +87,7 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
   const long f = blockIdx.x;
   const long long b = seg[f], e = seg[f + 1];
   double n = 0, cc = 0, cs = 0, ss = 0, cy = 0, sy = 0, yy = 0;
-  for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const double w = amask ? (double)__popc(amask[i]) : 1.0;
-    double s, c;
-    if (tab) {
-      const int g = gidx[i];
-      c = cs_tab[g];
-      s = cs_tab[G + g];
-    } else {
-      sincos(az[i], &s, &c);
-    }
-    const double yi = y[i];
+  auto acc1 = [&](double w, double c, double s, double yi) {
     n += w;
     cc += w * c * c;
     cs += w * c * s;
@@ -83,6 +95,24 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
     cy += w * c * yi;
     sy += w * s * yi;
     yy += w * yi * yi;
+  };
+  const long long step = (long long)blockDim.x * kVelU;
+  if (tab) {
+    // kVelU cells per thread per trip, all loads issued first: the loop is HBM-latency bound otherwise
+    for (long long i0 = b + threadIdx.x; i0 < e; i0 += step) {
+      int gv[kVelU];
+      double yv[kVelU];
+      unsigned mv[kVelU];
+      vel_load(i0, e, gidx, y, amask, gv, yv, mv);
+#pragma unroll
+      for (int u = 0; u < kVelU; ++u) acc1((double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+    }
+  } else {
+    for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
+      double s, c;
+      sincos(az[i], &s, &c);
+      acc1(amask ? (double)__popc(amask[i]) : 1.0, c, s, y[i]);
+    }
   }
   const double vals[7] = {n, cc, cs, ss, cy, sy, yy};
   for (int v = 0; v < 7; ++v) {
@@ -132,22 +162,31 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
   __syncthreads();
   const double vx = sol[0], vy = sol[1];
   double r2 = 0.0, rmax = 0.0;
-  for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const double w = amask ? (double)__popc(amask[i]) : 1.0;
-    double s, c;
-    if (tab) {
-      const int g = gidx[i];
-      c = cs_tab[g];
-      s = cs_tab[G + g];
-    } else {
-      sincos(az[i], &s, &c);
-    }
+  auto acc2 = [&](long long i, double w, double c, double s, double yi) {
     const double pr = k * (vx * c + vy * s);
-    const double r = y[i] - pr;
+    const double r = yi - pr;
     r2 += w * r * r;
     if (w > 0) rmax = fmax(rmax, fabs(r));
     if (resid) resid[i] = r;
     if (pred) pred[i] = pr;
+  };
+  if (tab) {
+    for (long long i0 = b + threadIdx.x; i0 < e; i0 += step) {
+      int gv[kVelU];
+      double yv[kVelU];
+      unsigned mv[kVelU];
+      vel_load(i0, e, gidx, y, amask, gv, yv, mv);
+#pragma unroll
+      for (int u = 0; u < kVelU; ++u)
+        if (i0 + (long long)u * blockDim.x < e)
+          acc2(i0 + (long long)u * blockDim.x, (double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+    }
+  } else {
+    for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
+      double s, c;
+      sincos(az[i], &s, &c);
+      acc2(i, amask ? (double)__popc(amask[i]) : 1.0, c, s, y[i]);
+    }
   }
   const double R2 = block_sum(r2, sh);
   const double RM = block_max(rmax, sh);
