@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
 // runs phases 1-2 in rounds of kEmitCap (a per-word store loop would scatter 4-byte stores: measured 2.9x HBM write
 // amplification on the 54%-dense cell unions of cfg2).
 constexpr int kEmitCap = 4096;
+constexpr int kEmitU = 4;  // phase-2 items per lane per trip
 
 RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -259,19 +260,20 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
                                                     int* __restrict__ e_cell, double* __restrict__ e_pdb,
                                                     int* __restrict__ c_frame, int* __restrict__ c_rc,
                                                     unsigned* __restrict__ c_amask) {
+  static_assert(64 % W == 0, "a mask row must lie within one wave");
   __shared__ unsigned pk[kEmitCap];   // item code: (word << 6) | bit
   __shared__ unsigned pam[kEmitCap];  // cells: antenna mask of the item
   __shared__ int wsum[4];
   __shared__ int s_loc[256], s_cw[256], s_r0[256], s_fi[256];
   __shared__ unsigned long long s_u[256];
   __shared__ long long s_first;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
   const bool entries = blockIdx.x < nblk_e;
   const long long nent = F * A * S * W, ncw = F * S * W;
-  const long long gw = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256 + t;
+  const long long gw0 = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256;  // row-aligned
   const long long nw = entries ? nent : ncw;
-  unsigned long long m = 0;
-  if (gw < nw) m = entries ? mask[gw] : umask[gw];
+  const bool valid = gw0 + t < nw;
+  const long long gw = valid ? gw0 + t : gw0;  // past-the-end words alias the block's first word (then m = 0)
   // word -> (row, w); entries: row = (f*A + a)*S + i, cells: row = f*S + i  (divisions once per word)
   const long long row = gw / W;
   const int w = (int)(gw - row * W);
@@ -279,45 +281,38 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   const int i = (int)(row - q * S);
   const long long f = entries ? q / A : q;
   const int a = entries ? (int)(q - f * A) : 0;
-  const int cnt = __popcll(m);
-  int total;
-  const int loc = block_exclusive_scan(cnt, wsum, total);
-  // the block's first item index: offsets of the first word (earlier words of its row included)
-  if (t == 0) {
-    long long fst;
-    if (entries) {
-      fst = entry_base[f] + entry_row_off[row];
-      for (int ww = 0; ww < w; ++ww) fst += __popcll(mask[row * W + ww]);
-    } else {
-      fst = cell_base[f] + cell_row_off[row];
-      for (int ww = 0; ww < w; ++ww) fst += __popcll(umask[row * W + ww]);
-    }
-    s_first = fst;
-  }
+  // every global load of the word is issued here, independent of its value (one memory round trip)
+  unsigned long long m = entries ? mask[gw] : umask[gw];
+  long long fst = 0;  // thread 0: the block's first item index (the block starts a row: no earlier words)
+  if (t == 0) fst = entries ? entry_base[f] + entry_row_off[row] : cell_base[f] + cell_row_off[row];
   unsigned long long u = 0;  // entries: the union word of (f, i, w)
-  int r0 = 0, cw = 0;
-  if (entries && m) {
+  long long cwb = 0;
+  int cwo = 0;
+  if (entries) {
     const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
-    cw = (int)(cell_base[f] + cell_row_off[f * S + i]);
+    u = urow[w];
+    cwb = cell_base[f] + cell_row_off[f * S + i];
 #pragma unroll
     for (int ww = 0; ww < W; ++ww)
-      if (ww < w) {
-        r0 += __popcll(mask[row * W + ww]);
-        cw += __popcll(urow[ww]);
-      }
-    u = urow[w];
+      if (ww < w) cwo += __popcll(urow[ww]);
   }
   unsigned long long ma[MAXA];  // cells: the antennas' peak words of (f, i, w)
-  if (!entries && m) {
+  if (!entries) {
 #pragma unroll
     for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
   }
+  if (!valid) m = 0;
+  const int cnt = __popcll(m);
+  int total;
+  const int loc = block_exclusive_scan(cnt, wsum, total);
+  // entries: peaks of the earlier words of this row (the row's words are lanes lane-w .. lane of this wave)
+  const int r0 = loc - __shfl(loc, lane - w);
+  if (t == 0) s_first = fst;
   s_loc[t] = loc;
   s_r0[t] = r0;
-  s_cw[t] = cw;
+  s_cw[t] = (int)(cwb + cwo);
   s_u[t] = u;
   s_fi[t] = entries ? ((a << 16) | i) : (int)f;
-  const long long gw0 = gw - t;  // first word of the block
   // rounds of kEmitCap items (one round unless the block is dense, e.g. the cell union at high peak density)
   for (int base = 0; base < total; base += kEmitCap) {
     // phase 1: packed (word, bit) codes (+ the cell's antenna mask) of this round's items, in LDS
@@ -342,29 +337,53 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
     __syncthreads();
     const long long first = s_first + base;
     const int nk = total - base < kEmitCap ? total - base : kEmitCap;
-    // phase 2: coalesced stores, lane k % 256 writes item k (no divisions: per-word data come from LDS)
-    for (int k = t; k < nk; k += 256) {
-      const unsigned code = pk[k];
-      const int tt = (int)(code >> 6), b = (int)(code & 63);
-      const long long g2 = gw0 + tt;
-      const int ww = (int)(g2 % W);
-      const long long e = first + k;
+    // phase 2: coalesced stores, lane k % 256 writes item k; kEmitU items per trip with their peak-power
+    // gathers issued first (a rolled loop waits on each gather in turn)
+    for (int k0 = t; k0 < nk; k0 += 256 * kEmitU) {
       if (entries) {
-        if (e < entry_cap) {
-          const int ai = s_fi[tt];
-          const int ii = ai & 0xffff;
-          const int r = s_r0[tt] + (base + k - s_loc[tt]);
-          e_ant[e] = ai >> 16;
-          e_rbin[e] = ii;
-          e_dbin[e] = ww * 64 + b;
-          e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
-          if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pk_pow[(size_t)(g2 / W) * C + r] + 1e-12f));  // dechirp.py:235-236
+        float pw[kEmitU];
+#pragma unroll
+        for (int uu = 0; uu < kEmitU; ++uu) {
+          const int k = k0 + 256 * uu;
+          pw[uu] = 0.f;
+          if (k < nk && e_pdb) {
+            const unsigned code = pk[k];
+            const int tt = (int)(code >> 6);
+            pw[uu] = pk_pow[(size_t)((gw0 + tt) / W) * C + s_r0[tt] + (base + k - s_loc[tt])];
+          }
         }
-      } else if (e < cell_cap) {
-        const long long rw = g2 / W;
-        c_frame[e] = s_fi[tt];
-        c_rc[e] = (int)(rw - (long long)s_fi[tt] * S) * C + ww * 64 + b;
-        c_amask[e] = pam[k];
+#pragma unroll
+        for (int uu = 0; uu < kEmitU; ++uu) {
+          const int k = k0 + 256 * uu;
+          const long long e = first + k;
+          if (k < nk && e < entry_cap) {
+            const unsigned code = pk[k];
+            const int tt = (int)(code >> 6), b = (int)(code & 63);
+            const int ww = (int)((gw0 + tt) % W);
+            const int ai = s_fi[tt];
+            e_ant[e] = ai >> 16;
+            e_rbin[e] = ai & 0xffff;
+            e_dbin[e] = ww * 64 + b;
+            e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
+            if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pw[uu] + 1e-12f));  // dechirp.py:235-236
+          }
+        }
+      } else {
+#pragma unroll
+        for (int uu = 0; uu < kEmitU; ++uu) {
+          const int k = k0 + 256 * uu;
+          const long long e = first + k;
+          if (k < nk && e < cell_cap) {
+            const unsigned code = pk[k];
+            const int tt = (int)(code >> 6), b = (int)(code & 63);
+            const long long g2 = gw0 + tt;
+            const long long rw = g2 / W;
+            const int ww = (int)(g2 - rw * W);
+            c_frame[e] = s_fi[tt];
+            c_rc[e] = (int)(rw - (long long)s_fi[tt] * S) * C + ww * 64 + b;
+            c_amask[e] = pam[k];
+          }
+        }
       }
     }
     __syncthreads();  // pk / pam reused by the next round
