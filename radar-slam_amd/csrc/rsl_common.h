@@ -175,7 +175,7 @@ constexpr int lp_row(int N) { return N + (N + 7) / 8; }
 // One Stockham autosort stage over ROWS independent rows of N points held in LDS
 // (row stride LD complex, padded positions).  tw[k] = exp(-2 pi i k / N), k < N (fp64-accurate table).
 // In place: every thread reads its butterflies' inputs, the block syncs, then writes.
-template <int N, int R, int NS, int ROWS, int NT, int LD>
+template <int N, int R, int NS, int ROWS, int NT, int LD, bool PADTW>
 RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
   constexpr int NB = N / R;
   constexpr int TOT = ROWS * NB;
@@ -207,7 +207,7 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
       if (NS > 1) {
         constexpr int STEP = N / (NS * R);
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[r * k * STEP]);
+        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[PADTW ? lp(r * k * STEP) : r * k * STEP]);
       }
       Dft<R>::run(v[q]);
       float2* dst = buf + row * LD;
@@ -230,21 +230,23 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
   __syncthreads();
 }
 
-template <int N, int S, int ROWS, int NT, int LD>
+template <int N, int S, int ROWS, int NT, int LD, bool PADTW>
 RSL_DEV void fft_run(float2* buf, const float2* tw, int tid) {
   constexpr FftPlan P = make_plan(N);
   if constexpr (S < P.n) {
-    fft_stage<N, P.r[S], P.ns[S], ROWS, NT, LD>(buf, tw, tid);
-    fft_run<N, S + 1, ROWS, NT, LD>(buf, tw, tid);
+    fft_stage<N, P.r[S], P.ns[S], ROWS, NT, LD, PADTW>(buf, tw, tid);
+    fft_run<N, S + 1, ROWS, NT, LD, PADTW>(buf, tw, tid);
   }
 }
 
 // Forward N-point FFT of ROWS rows in LDS (padded positions, see lp()).  Caller must __syncthreads() before.
-template <int N, int ROWS, int NT, int LD>
+// PADTW: the twiddle table is stored at padded positions lp(k) (spreads the strided twiddle reads of the
+// later stages over the LDS banks)
+template <int N, int ROWS, int NT, int LD, bool PADTW = false>
 RSL_DEV void fft_rows(float2* buf, const float2* tw, int tid) {
   static_assert(make_plan(N).n > 0, "unsupported FFT size");
   static_assert(LD >= lp_row(N), "row stride too small for the padded layout");
-  fft_run<N, 0, ROWS, NT, LD>(buf, tw, tid);
+  fft_run<N, 0, ROWS, NT, LD, PADTW>(buf, tw, tid);
 }
 
 // ESPRIT closed form (reference angle_estimation.py:178-225) on a unit-norm fp64 signature s (A antennas):

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
 // (no RDS re-read), 10 log10 in fp32 (the powers are fp32), stored as float64 like power_spectrum_db.  A block with more than kEmitCap items
 // runs phases 1-2 in rounds of kEmitCap (a per-word store loop would scatter 4-byte stores: measured 2.9x HBM write
 // amplification on the 54%-dense cell unions of cfg2).
-constexpr int kEmitCap = 4096;
+constexpr int kEmitCap = 2048;
 constexpr int kEmitU = 4;  // phase-2 items per lane per trip
 
 RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {

@@ -223,9 +223,13 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        uint4 oh, ol, xh, xl;
-        split8(e + 16 * kb + 8 * h, oh, ol);        // own cell, K rows 8h..8h+7
-        split8(e + 16 * kb + 8 * (1 - h), xh, xl);  // own cell, the partner's K half
+        // both K halves split with static register indices, then selected by h (an index into e[] that
+        // depends on the lane becomes a compare/select chain per element)
+        uint4 h0h, h0l, h1h, h1l;
+        split8(e + 16 * kb, h0h, h0l);
+        split8(e + 16 * kb + 8, h1h, h1l);
+        const uint4 oh = sel_u4(h == 0, h0h, h1h), ol = sel_u4(h == 0, h0l, h1l);  // own cell, K rows 8h..8h+7
+        const uint4 xh = sel_u4(h == 0, h1h, h0h), xl = sel_u4(h == 0, h1l, h0l);  // own cell, partner's K half
         const uint4 rh = shfl_xor32_u4(xh), rl = shfl_xor32_u4(xl);  // partner's cell, K rows 8h..8h+7
         b0h[kb] = sel_u4(h == 0, oh, rh);
         b0l[kb] = sel_u4(h == 0, ol, rl);

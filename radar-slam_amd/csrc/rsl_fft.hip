@@ -122,10 +122,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
   static_assert((CB * H) % kThreads == 0, "tile must split evenly over the block");
   extern __shared__ float2 sm[];
   float2* tws = sm;
-  float2* buf = sm + S;
+  float2* buf = sm + lp_row(S);
   const int tid = threadIdx.x;
   const int ncb = (C + CB - 1) / CB;
-  for (int k = tid; k < S; k += kThreads) tws[k] = tw[k];
+  for (int k = tid; k < S; k += kThreads) tws[lp(k)] = tw[k];
   const float4* tab4 = reinterpret_cast<const float4*>(table);
   float4 tab[PF];
 #pragma unroll
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
     }
     __syncthreads();
     if (t + gridDim.x < ntile) load(t + gridDim.x);  // in flight during the FFT below
-    fft_rows<S, CB, kThreads, LD>(buf, tws, tid);
+    fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);
     if (dc) {
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
       __syncthreads();
@@ -440,7 +440,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     auto go = [&](auto cbc) -> hipError_t {
       constexpr int CBX = decltype(cbc)::value;
       const long ntile = (long)F * A * ((C + CBX - 1) / CBX);
-      const size_t lds = sizeof(float2) * (S + (size_t)CBX * lp_row(S));
+      const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CBX * lp_row(S));
       const long nblk = resident_grid(reinterpret_cast<const void*>(k_range_fft_p<S, CBX>), lds, ntile);
       hipLaunchKernelGGL((k_range_fft_p<S, CBX>), dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C,
                          ntile, table, tw, dc, work);
