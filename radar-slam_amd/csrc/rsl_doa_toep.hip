@@ -19,6 +19,7 @@
 // MUSIC rule (angle_estimation.py:149-152): the spectrum is 1/(M - P) if M - P > 1e-12 else 0.  That can
 // only change the argmax when max P is within rounding of M (s equal to a steering vector).  Such cells
 // are re-scanned exactly in fp64 from the reference's fp64 steering table (rare, lane-divergent path).
+#include <climits>
 #include <cstdlib>
 
 #include "rsl_common.h"
@@ -92,12 +93,18 @@ RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ 
   }
 }
 
-// Max of one 32x32 tile's 16 values held by this lane (v_max3 tree; fmaxf returns one of its inputs exactly).
+// Max of one 32x32 tile's 16 values held by this lane, as signed-integer max3 on the float bits (v_max3_i32):
+// order-preserving for non-negative floats, and a tile max is one of its inputs exactly.  P = |a^H s|^2 >= 0; a
+// rounding-negative value can only lose to a positive one, and a tile whose values are all <= 0 never holds the
+// spectrum maximum of a non-zero signature.  (fmaxf on MFMA outputs costs NaN-canonicalising v_max_f32 ops.)
 RSL_DEV float tile_max(const floatx16& a) {
-  const float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
-  const float m2 = fmaxf(fmaxf(a[6], a[7]), a[8]), m3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
-  const float m4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
-  return fmaxf(fmaxf(fmaxf(m0, m1), m2), fmaxf(fmaxf(m3, m4), a[15]));
+  int v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = __float_as_int(a[i]);
+  auto mx3 = [](int x, int y, int z) { return max(max(x, y), z); };
+  const int m0 = mx3(v[0], v[1], v[2]), m1 = mx3(v[3], v[4], v[5]), m2 = mx3(v[6], v[7], v[8]);
+  const int m3 = mx3(v[9], v[10], v[11]), m4 = mx3(v[12], v[13], v[14]);
+  return __int_as_float(mx3(mx3(m0, m1, m2), mx3(m3, m4, v[15]), INT_MIN));
 }
 
 // Exact fp64 scan of one cell (MUSIC near-degenerate path): key = P if M - P > 1e-12 else -1, first index.
