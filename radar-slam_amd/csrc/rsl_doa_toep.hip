@@ -39,7 +39,9 @@ RSL_DEV void toep_entries(const float2 (&s)[MA], float (&e)[16 * KB]) {
   float pw = 0.f;
 #pragma unroll
   for (int m = 0; m < MA; ++m) pw = fmaf(s[m].x, s[m].x, fmaf(s[m].y, s[m].y, pw));
-  const float inv = pw > 0.f ? kToepScale / pw : 0.f;  // angle_estimation.py:86-88 (unit-norm s)
+  // angle_estimation.py:86-88 (unit-norm s).  v_rcp_f32 (1 ulp): a common scale of all of a cell's grid values
+  // cannot move its argmax, and the MUSIC degeneracy test has a 1e-4 margin
+  const float inv = pw > 0.f ? kToepScale * __builtin_amdgcn_rcpf(pw) : 0.f;
   e[0] = pw > 0.f ? kToepScale : 0.f;
 #pragma unroll
   for (int k = 1; k < MA; ++k) {
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
     if constexpr (EXTRAS) {
       // fused K6 (k_cell_extras) for the own cell, before the scan so its registers are dead during the MFMA
       // loop: ESPRIT (angle_estimation.py:178-225) and the spatial phase angle(s1 conj(s0)) (velocity_solver.py
-      // :136); fp32 closed form from the fp32 signature, fp64 asin.
+      // :136); fp32 closed form from the fp32 signature.
       float sr[MA], si[MA], pw = 0.f;
 #pragma unroll
       for (int m = 0; m < MA; ++m) {
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
         pw = fmaf(sr[m], sr[m], fmaf(si[m], si[m], pw));
       }
       if (pw > 0.f) {
-        const float sc = 1.0f / sqrtf(pw);
+        const float sc = __builtin_amdgcn_rsqf(pw);  // ESPRIT and the phase are invariant to the scale
 #pragma unroll
         for (int m = 0; m < MA; ++m) {
           sr[m] *= sc;
@@ -213,7 +215,12 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
           float nr, ni, dd;
           esprit_phi<MA>(sr, si, A, nr, ni, dd);
           const float ang = dd > 0.f ? atan2f(ni, nr) : 0.f;
-          out_esprit[c] = asin((double)ang * esprit_scale) * (180.0 / 3.14159265358979323846);
+          // fp32 asin (the input angle is fp32 already; tolerance 1e-3 rad).  For d >= lambda/2 the reference's
+          // argument never exceeds 1 (|angle| <= pi): clamp the fp32 rounding of pi * scale there; for d < lambda/2
+          // |x| > 1 gives NaN as in the reference.
+          float x = ang * (float)esprit_scale;
+          if (esprit_scale * 3.14159265358979323846 <= 1.0 + 1e-9) x = fminf(fmaxf(x, -1.f), 1.f);
+          out_esprit[c] = (double)(asinf(x) * 57.2957795130823208768f);
         }
         if (out_phase) out_phase[c] = (double)atan2f(si[1] * sr[0] - sr[1] * si[0], sr[1] * sr[0] + si[1] * si[0]);
       }
