@@ -29,6 +29,20 @@ constexpr FftPlan make_plan(int N) {
   FftPlan p{0, {}, {}};
   int m = N;
   int ns = 1;
+  // powers of two: radix 8 stages, with one radix-16 stage where it removes a stage (N = 16 * 8^k: 128, 1024)
+  // or two where they replace 8 * 8 * 4 (N = 256); every stage is an LDS round trip
+  int lg = 0;
+  while ((1 << lg) < N) ++lg;
+  if ((1 << lg) == N && N >= 128) {
+    const int n16 = (lg % 3 == 1) ? 1 : (N == 256 ? 2 : 0);
+    for (int q = 0; q < n16; ++q) {
+      p.r[p.n] = 16;
+      p.ns[p.n] = ns;
+      ns *= 16;
+      m /= 16;
+      p.n++;
+    }
+  }
   const int order[6] = {8, 4, 2, 5, 3, 7};
   for (int oi = 0; oi < 6; ++oi) {
     int R = order[oi];
@@ -92,6 +106,39 @@ struct Dft<8> {
     for (int k = 0; k < 4; ++k) {
       v[2 * k] = e[k];
       v[2 * k + 1] = o[k];
+    }
+  }
+};
+
+// 16 points as 4 x 4: n = 4 n1 + n2, k = k1 + 4 k2; DFT4 over n1, twiddle W16^(n2 k1), DFT4 over n2.
+template <>
+struct Dft<16> {
+  RSL_DEV static void run(float2* v) {
+    const float h = 0.70710678118654752440f, c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    float2 y[4][4];  // y[n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+      float2 t[4] = {v[n2], v[4 + n2], v[8 + n2], v[12 + n2]};
+      Dft<4>::run(t);
+#pragma unroll
+      for (int k1 = 0; k1 < 4; ++k1) y[n2][k1] = t[k1];
+    }
+    // W16^e, e = n2 k1: 1 = (c, -s), 2 = (h, -h), 3 = (s, -c), 4 = -i, 6 = (-h, -h), 9 = (-c, s)
+    y[1][1] = cmul(y[1][1], make_float2(c1, -s1));
+    y[1][2] = make_float2(h * (y[1][2].x + y[1][2].y), h * (y[1][2].y - y[1][2].x));
+    y[1][3] = cmul(y[1][3], make_float2(s1, -c1));
+    y[2][1] = make_float2(h * (y[2][1].x + y[2][1].y), h * (y[2][1].y - y[2][1].x));
+    y[2][2] = cmul_mi(y[2][2]);
+    y[2][3] = make_float2(h * (y[2][3].y - y[2][3].x), -h * (y[2][3].x + y[2][3].y));
+    y[3][1] = cmul(y[3][1], make_float2(s1, -c1));
+    y[3][2] = make_float2(h * (y[3][2].y - y[3][2].x), -h * (y[3][2].x + y[3][2].y));
+    y[3][3] = cmul(y[3][3], make_float2(-c1, s1));
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      float2 t[4] = {y[0][k1], y[1][k1], y[2][k1], y[3][k1]};
+      Dft<4>::run(t);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = t[k2];
     }
   }
 };
@@ -212,11 +259,11 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
       Dft<R>::run(v[q]);
       float2* dst = buf + row * LD;
       const int o = (j / NS) * NS * R + k;
-      if constexpr (NS == 1 && R <= 8 && (R & (R - 1)) == 0) {
-        // o = j R: the R outputs never cross a pad slot, lp(o + r) = lp(o) + r
+      if constexpr (NS == 1 && (R & (R - 1)) == 0 && (R <= 8 || R % 8 == 0)) {
+        // o = j R (a multiple of 8 or of R): lp(o + r) = lp(o) + r + r / 8
         float2* d0 = dst + lp(o);
 #pragma unroll
-        for (int r = 0; r < R; ++r) d0[r] = v[q][r];
+        for (int r = 0; r < R; ++r) d0[r + (r >> 3)] = v[q][r];
       } else if constexpr (NS % 8 == 0) {
         float2* d0 = dst + lp(o);
 #pragma unroll
