@@ -218,11 +218,17 @@ RSL_DEV long xcd_tile(long b, long n) {
 RSL_DEV constexpr int lp(int x) { return x + (x >> 3); }
 // Padded row length for N points.
 constexpr int lp_row(int N) { return N + (N + 7) / 8; }
+// The same with the padding optional (P = false: plain rows, for kernels whose FFT is not LDS-bound and that
+// need the smaller tile for residency)
+template <bool P>
+RSL_DEV constexpr int lpp(int x) { return P ? x + (x >> 3) : x; }
+template <bool P>
+constexpr int lp_rowp(int N) { return P ? lp_row(N) : N; }
 
 // One Stockham autosort stage over ROWS independent rows of N points held in LDS
 // (row stride LD complex, padded positions).  tw[k] = exp(-2 pi i k / N), k < N (fp64-accurate table).
 // In place: every thread reads its butterflies' inputs, the block syncs, then writes.
-template <int N, int R, int NS, int ROWS, int NT, int LD, bool PADTW>
+template <int N, int R, int NS, int ROWS, int NT, int LD, bool PADTW, bool PAD>
 RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
   constexpr int NB = N / R;
   constexpr int TOT = ROWS * NB;
@@ -234,10 +240,10 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
     if ((TOT % NT) == 0 || idx < TOT) {
       const int row = idx / NB, j = idx - (idx / NB) * NB;
       const float2* src = buf + row * LD;
-      if constexpr (NB % 8 == 0) {  // lp(j + r NB) = lp(j) + r (NB + NB/8): immediate LDS offsets
-        const float2* s0 = src + lp(j);
+      if constexpr (NB % 8 == 0 || !PAD) {  // lp(j + r NB) = lp(j) + r (NB + NB/8): immediate LDS offsets
+        const float2* s0 = src + lpp<PAD>(j);
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[q][r] = s0[r * (NB + NB / 8)];
+        for (int r = 0; r < R; ++r) v[q][r] = s0[r * lpp<PAD>(NB)];
       } else {
 #pragma unroll
         for (int r = 0; r < R; ++r) v[q][r] = src[lp(j + r * NB)];
@@ -259,7 +265,11 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
       Dft<R>::run(v[q]);
       float2* dst = buf + row * LD;
       const int o = (j / NS) * NS * R + k;
-      if constexpr (NS == 1 && (R & (R - 1)) == 0 && (R <= 8 || R % 8 == 0)) {
+      if constexpr (!PAD) {
+        float2* d0 = dst + o;
+#pragma unroll
+        for (int r = 0; r < R; ++r) d0[r * NS] = v[q][r];
+      } else if constexpr (NS == 1 && (R & (R - 1)) == 0 && (R <= 8 || R % 8 == 0)) {
         // o = j R (a multiple of 8 or of R): lp(o + r) = lp(o) + r + r / 8
         float2* d0 = dst + lp(o);
 #pragma unroll
@@ -277,23 +287,24 @@ RSL_DEV void fft_stage(float2* buf, const float2* tw, int tid) {
   __syncthreads();
 }
 
-template <int N, int S, int ROWS, int NT, int LD, bool PADTW>
+template <int N, int S, int ROWS, int NT, int LD, bool PADTW, bool PAD>
 RSL_DEV void fft_run(float2* buf, const float2* tw, int tid) {
   constexpr FftPlan P = make_plan(N);
   if constexpr (S < P.n) {
-    fft_stage<N, P.r[S], P.ns[S], ROWS, NT, LD, PADTW>(buf, tw, tid);
-    fft_run<N, S + 1, ROWS, NT, LD, PADTW>(buf, tw, tid);
+    fft_stage<N, P.r[S], P.ns[S], ROWS, NT, LD, PADTW, PAD>(buf, tw, tid);
+    fft_run<N, S + 1, ROWS, NT, LD, PADTW, PAD>(buf, tw, tid);
   }
 }
 
 // Forward N-point FFT of ROWS rows in LDS (padded positions, see lp()).  Caller must __syncthreads() before.
 // PADTW: the twiddle table is stored at padded positions lp(k) (spreads the strided twiddle reads of the
 // later stages over the LDS banks)
-template <int N, int ROWS, int NT, int LD, bool PADTW = false>
+// PAD = false: rows hold points at plain positions (row stride LD >= N).
+template <int N, int ROWS, int NT, int LD, bool PADTW = false, bool PAD = true>
 RSL_DEV void fft_rows(float2* buf, const float2* tw, int tid) {
   static_assert(make_plan(N).n > 0, "unsupported FFT size");
-  static_assert(LD >= lp_row(N), "row stride too small for the padded layout");
-  fft_run<N, 0, ROWS, NT, LD, PADTW>(buf, tw, tid);
+  static_assert(LD >= lp_rowp<PAD>(N), "row stride too small for the row layout");
+  fft_run<N, 0, ROWS, NT, LD, PADTW, PAD>(buf, tw, tid);
 }
 
 // ESPRIT closed form (reference angle_estimation.py:178-225) on a unit-norm fp64 signature s (A antennas):

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-template <int C, int KB, int NT>
+template <int C, int KB, int NT, bool PAD, int DBG = 0>
 __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
                                                              float thr_f, int i_lo, int i_hi,
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
                                                              int* __restrict__ row_count, float* __restrict__ dbmap,
                                                              float* __restrict__ pk_pow, int xcd) {
   constexpr int NR = KB + 2;
-  constexpr int LD = lp_row(C) | 1;  // odd: conflict-free transposed (column) writes
+  constexpr int LD = lp_rowp<PAD>(C) | 1;  // odd: conflict-free transposed (column) writes
   constexpr int W = (C + 63) / 64;
   constexpr int PER = (NR * C + NT - 1) / NT;
   extern __shared__ float2 sm[];
@@ -280,15 +280,15 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 #pragma unroll
     for (int q = 0; q < TWP; ++q)
       if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
-    float2* row = buf + (ri + 1) * LD + lp(cs);
+    float2* row = buf + (ri + 1) * LD + lpp<PAD>(cs);
 #pragma unroll
-    for (int q = 0; q < PI; ++q) row[q * CS + ((q * CS) >> 3)] = ld[q];
+    for (int q = 0; q < PI; ++q) row[lpp<PAD>(q * CS)] = ld[q];
 #pragma unroll
     for (int h = 0; h < PH; ++h) {
       const int e = tid + h * NT;
       if ((2 * C) % NT == 0 || e < 2 * C) {
         const int side = e / C, c = e - side * C;
-        buf[(side ? NR - 1 : 0) * LD + lp(c)] = ld[PI + h];
+        buf[(side ? NR - 1 : 0) * LD + lpp<PAD>(c)] = ld[PI + h];
       }
     }
   } else {
@@ -311,12 +311,12 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
       const int idx = tid + q * NT;
       if ((NR * C) % NT == 0 || idx < NR * C) {
         const int c = idx / NR, r = idx - c * NR;
-        buf[r * LD + lp(c)] = ld[q];
+        buf[r * LD + lpp<PAD>(c)] = ld[q];
       }
     }
   }
   __syncthreads();
-  fft_rows<C, NR, NT, LD>(buf, tws, tid);
+  if constexpr (DBG != 1) fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);  // DBG 1: no FFT (ablation)
   const int hs = S / 2, hc = C / 2;
   int i0 = k0 + hs;  // shifted row of LDS row 1
   if (i0 >= S) i0 -= S;
@@ -331,8 +331,8 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
       const int r = idx / C, j = idx - r * C;  // j: shifted doppler index
       int d = j - hc;                          // out[j] = X[(j - C//2) mod C]
       if (d < 0) d += C;
-      const float2 z = buf[r * LD + lp(d)];
-      if (r >= 1 && r <= KB) dst[(size_t)(r - 1) * C + j] = z;
+      const float2 z = buf[r * LD + lpp<PAD>(d)];
+      if (DBG != 2 && r >= 1 && r <= KB) dst[(size_t)(r - 1) * C + j] = z;  // DBG 2: no RDS store
       pr[q] = cabs2(z);
     }
   }
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  for (int kk = wave; kk < KB; kk += NT / 64) {
+  for (int kk = wave; kk < (DBG == 3 ? 0 : KB); kk += NT / 64) {  // DBG 3: no detection
     const int i = i0 + kk;
     const bool gate = (i >= i_lo && i <= i_hi);
     const bool has_up = i > 0, has_dn = i + 1 < S;
@@ -389,15 +389,26 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
                                 int* row_count, float* dbmap, float* pk_pow) {
   const long ntile = (long)F * A * (S / KB);
-  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * (lp_row(C) | 1));
+  // padded LDS rows; RSL_DD_PAD=0 selects plain rows (smaller tile: measured slower, 2.14 vs 1.98 ms per 1000
+  // cfg2 frames, also with the registers capped for 8 resident workgroups per CU)
+  const char* pe = getenv("RSL_DD_PAD");
+  const bool pad = !pe || atoi(pe) != 0;
+  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * ((pad ? lp_row(C) : C) | 1));
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
   // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
   // 256 threads (a 320-thread block that runs each radix-8 stage of the 18-row KB-16 tile in one pass measured
   // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
   constexpr int NT = 256;
-  hipLaunchKernelGGL((k_doppler_detect<C, KB, NT>), dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds,
-                     thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow, dd_xcd());
+  auto kern = pad ? k_doppler_detect<C, KB, NT, true> : k_doppler_detect<C, KB, NT, false>;
+  if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (timing only: results are wrong)
+    const int v = atoi(e);
+    if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1>;
+    if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2>;
+    if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3>;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds, thr_f, i_lo, i_hi, mask,
+                     row_count, dbmap, pk_pow, dd_xcd());
   return hipGetLastError();
 }
 
