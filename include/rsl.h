@@ -81,10 +81,14 @@ int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double
 
 /* a7 + a8 fused: range FFT, then Doppler FFT + fftshift + RDS store + peak detection in one kernel (the RDS is
  *     not re-read for detection).  Arguments as rsl_rds and rsl_detect; falls back to the two calls when the
- *     shape is not covered (C not a power of two <= 1024, or its range-bin tiling does not divide S/2). */
+ *     shape is not covered (C not a power of two <= 1024, or its range-bin tiling does not divide S/2).
+ *     peak_pow is written group-compact: the peaks of the G rows r0 .. r0+G-1 of one (frame, antenna)
+ *     (row = (f*A + a)*S + i, r0 a multiple of G) are contiguous from slot r0*C, in row order and Doppler order
+ *     within a row (full cache lines instead of a short run per row).  *peak_pow_group (host, nullable)
+ *     receives G (1 = row-compact, as rsl_detect writes it); pass it to rsl_peak_emit. */
 int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
-                   void* mask, void* row_count, void* db_map, void* peak_pow);
+                   void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group);
 
 /* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
  * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
@@ -98,10 +102,11 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
 /* Emit the peak entries (e_* arrays, i32; e_pdb f64 = per-entry power_db, nullable) and the unique cells
  * (c_frame i32, c_rc i32 = range_bin*C + doppler_bin, c_amask u32 = antennas with a peak there).
  * e_cell maps each entry to its cell.  Items beyond *_cap are dropped (compare the totals).
- * With union_mask (from rsl_peak_offsets) and peak_pow (from rsl_detect) the RDS is not read (rds may be
- * NULL); otherwise power_db is recomputed from rds. */
-int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow, int F,
-                  int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
+ * With union_mask (from rsl_peak_offsets) and peak_pow (from rsl_detect / rsl_rds_detect, in the row grouping
+ * peak_pow_group those report; 1 for rsl_detect) the RDS is not read (rds may be NULL); otherwise power_db is
+ * recomputed from rds. */
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow,
+                  int peak_pow_group, int F, int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
                   const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
                   void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
 

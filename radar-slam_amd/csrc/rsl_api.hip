@@ -206,8 +206,9 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
 
 int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
-                   void* mask, void* row_count, void* db_map, void* peak_pow) {
+                   void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group) {
   if (!h) return RSL_ERR_INVALID;
+  if (peak_pow_group) *peak_pow_group = 1;
   if (!mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: null pointer");
   if (!rsl::doppler_detect_supported(C, S) || A <= 0 || F < 0) {  // unfused: a7 then a8
     if (int r = rsl_rds(h, cube, F, A, C_total, chirp0, C, S, table, dc_removal, work, rds)) return r;
@@ -222,6 +223,7 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   float2* tC = twiddles(h, C);
   if (!tS || !tC) return fail(h, RSL_ERR_HIP, "twiddle table allocation failed");
   bool sup = true;
+  int group = 1;
   hipError_t e;
   {
     Scope sc(h, RSL_K_RANGE_FFT);
@@ -233,8 +235,9 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
     Scope sc(h, RSL_K_DOPPLER_FFT);
     e = rsl::launch_doppler_detect(h->stream, (const float2*)work, F, A, C, S, tC, (float2*)rds, thr_power, i_lo,
                                    i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
-                                   (float*)peak_pow, &sup);
+                                   (float*)peak_pow, &sup, &group);
   }
+  if (peak_pow_group) *peak_pow_group = group;
   return hip_check(h, e, "doppler_detect");
 }
 
@@ -274,8 +277,8 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
                    "offsets");
 }
 
-int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow, int F,
-                  int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
+int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow,
+                  int peak_pow_group, int F, int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
                   const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
                   void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
   if (!h) return RSL_ERR_INVALID;
@@ -285,11 +288,14 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* u
   if ((entry_cap > 0 && (!e_ant || !e_rbin || !e_dbin || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null output");
   const int W = (C + 63) / 64;
+  if (peak_pow && (peak_pow_group < 1 || S % peak_pow_group != 0))
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: peak_pow_group must divide S");
   Scope sc(h, RSL_K_EMIT);
   if (union_mask && (peak_pow || !e_pdb) && (W & (W - 1)) == 0 && W <= 64)
     return hip_check(h,
                      rsl::launch_emit2(h->stream, (const unsigned long long*)mask,
-                                       (const unsigned long long*)union_mask, (const float*)peak_pow, F, A, S, C,
+                                       (const unsigned long long*)union_mask, (const float*)peak_pow,
+                                       peak_pow_group, F, A, S, C,
                                        (const int*)entry_row_off, (const int*)cell_row_off,
                                        (const long long*)entry_base, (const long long*)cell_base, entry_cap, cell_cap,
                                        (int*)e_ant, (int*)e_rbin, (int*)e_dbin, (int*)e_cell, (double*)e_pdb,

@@ -250,8 +250,8 @@ RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
 template <int W, int MAXA>
 __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __restrict__ mask,
                                                     const unsigned long long* __restrict__ umask,
-                                                    const float* __restrict__ pk_pow, long long F, int A, int S,
-                                                    int C, const int* __restrict__ entry_row_off,
+                                                    const float* __restrict__ pk_pow, int pk_group, long long F,
+                                                    int A, int S, int C, const int* __restrict__ entry_row_off,
                                                     const int* __restrict__ cell_row_off,
                                                     const long long* __restrict__ entry_base,
                                                     const long long* __restrict__ cell_base, long long entry_cap,
@@ -288,7 +288,10 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   unsigned long long u = 0;  // entries: the union word of (f, i, w)
   long long cwb = 0;
   int cwo = 0;
+  int gof = 0;  // entries: peaks of the earlier rows of the row's peak_pow group
   if (entries) {
+    const int ig = i - i % pk_group;
+    if (ig != i) gof = entry_row_off[row] - entry_row_off[row - (i - ig)];
     const unsigned long long* urow = umask + ((size_t)f * S + i) * W;
     u = urow[w];
     cwb = cell_base[f] + cell_row_off[f * S + i];
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   const int r0 = loc - __shfl(loc, lane - w);
   if (t == 0) s_first = fst;
   s_loc[t] = loc;
-  s_r0[t] = r0;
+  s_r0[t] = r0 + gof;
   s_cw[t] = (int)(cwb + cwo);
   s_u[t] = u;
   s_fi[t] = entries ? ((a << 16) | i) : (int)f;
@@ -349,7 +352,9 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
           if (k < nk && e_pdb) {
             const unsigned code = pk[k];
             const int tt = (int)(code >> 6);
-            pw[uu] = pk_pow[(size_t)((gw0 + tt) / W) * C + s_r0[tt] + (base + k - s_loc[tt])];
+            const long long rw = (gw0 + tt) / W;  // row (f A + a) S + i; its group's first row holds slot 0
+            const long long rg = rw - (rw % S) % pk_group;
+            pw[uu] = pk_pow[(size_t)rg * C + s_r0[tt] + (base + k - s_loc[tt])];
           }
         }
 #pragma unroll
@@ -391,7 +396,7 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
 }
 
 hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
-                        const float* pk_pow, int F, int A, int S, int C, const int* entry_row_off,
+                        const float* pk_pow, int pk_group, int F, int A, int S, int C, const int* entry_row_off,
                         const int* cell_row_off, const long long* entry_base, const long long* cell_base,
                         long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
                         double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
@@ -402,7 +407,7 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   const unsigned nb = (unsigned)(nbe + nbc);
 #define GO(WW)                                                                                                   \
   hipLaunchKernelGGL((A <= 8 ? k_emit_block<WW, 8> : k_emit_block<WW, 32>), dim3(nb), dim3(256), 0, st, mask,    \
-                     umask, pk_pow, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
+                     umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
                      entry_cap, cell_cap, nbe, e_ant, e_rbin, e_dbin, e_cell, e_pdb, c_frame, c_rc, c_amask);
   switch (W) {
     case 1: GO(1) break;

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
   __syncthreads();
   const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, n = lane & 31;
+  const int h = lane >> 5;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
   const long long nch = (ncell + 63) >> 6;
   const long long stride = (long long)gridDim.x * 4;

@@ -219,6 +219,172 @@ __global__ __launch_bounds__(kThreads) void k_doppler_fft(const float2* __restri
   }
 }
 
+// Tile body after the LDS fill (and its barrier): Doppler FFT, shifted RDS store, |X|^2 tile, 3x3 detection.
+template <int C, int KB, int NT, bool PAD, int DBG>
+RSL_DEV void dd_tile_compute(float2* buf, const float2* tws, int S, int k0, unsigned fa, float2* __restrict__ rds,
+                             float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
+                             int* __restrict__ row_count, float* __restrict__ dbmap, float* __restrict__ pk_pow) {
+  constexpr int NR = KB + 2;
+  constexpr int LD = lp_rowp<PAD>(C) | 1;
+  constexpr int W = (C + 63) / 64;
+  constexpr int PER = (NR * C + NT - 1) / NT;
+  const int tid = threadIdx.x;
+  if constexpr (DBG != 1) fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);  // DBG 1: no FFT (ablation)
+  const int hs = S / 2, hc = C / 2;
+  int i0 = k0 + hs;  // shifted row of LDS row 1
+  if (i0 >= S) i0 -= S;
+  float2* dst = rds + ((size_t)fa * S + i0) * C;
+  // one pass over the tile: shifted RDS stores (interior rows) and |X|^2 kept in registers
+  float pr[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    pr[q] = 0.f;
+    if (idx < NR * C) {
+      const int r = idx / C, j = idx - r * C;  // j: shifted doppler index
+      int d = j - hc;                          // out[j] = X[(j - C//2) mod C]
+      if (d < 0) d += C;
+      const float2 z = buf[r * LD + lpp<PAD>(d)];
+      if (DBG != 2 && r >= 1 && r <= KB) dst[(size_t)(r - 1) * C + j] = z;  // DBG 2: no RDS store
+      pr[q] = cabs2(z);
+    }
+  }
+  __syncthreads();
+  float* pw = reinterpret_cast<float*>(buf);  // power tile [NR][C], shifted doppler order
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = tid + q * NT;
+    if (idx < NR * C) pw[idx] = pr[q];
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int kk = wave; kk < (DBG == 3 ? 0 : KB); kk += NT / 64) {  // DBG 3: no detection
+    const int i = i0 + kk;
+    const bool gate = (i >= i_lo && i <= i_hi);
+    const bool has_up = i > 0, has_dn = i + 1 < S;
+    const float* up = pw + kk * C;
+    const float* mid = up + C;
+    const float* dn = mid + C;
+    const size_t row = (size_t)fa * S + i;
+    int cnt = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int j = w * 64 + lane;
+      bool pk = false;
+      float p = 0.f;
+      if (j < C) {
+        // 3x3 window max with 'reflect' edges (an out-of-range neighbour repeats an in-window cell)
+        const int jl = j > 0 ? j - 1 : j, jr = j + 1 < C ? j + 1 : j;
+        p = mid[j];
+        float m = fmaxf(fmaxf(mid[jl], p), mid[jr]);
+        if (has_up) m = fmaxf(m, fmaxf(fmaxf(up[jl], up[j]), up[jr]));
+        if (has_dn) m = fmaxf(m, fmaxf(fmaxf(dn[jl], dn[j]), dn[jr]));
+        pk = gate && (p > thr_f) && (p >= m);
+        if (dbmap) dbmap[row * C + j] = 10.f * log10f(p + 1e-12f);
+      }
+      const unsigned long long b = __ballot(pk);
+      if (lane == 0) mask[row * W + w] = b;
+      if (pk_pow && pk) pk_pow[row * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = p;
+      cnt += __popcll(b);
+    }
+    if (lane == 0) row_count[row] = cnt;
+  }
+}
+
+// Register form of the tile body for C = 64 NCH and KB = 8 NRH with NCH * NRH waves: wave (ch, rh) owns Doppler
+// columns 64 ch + lane and interior rows 8 rh + 1 .. 8 rh + 8.  Each lane reads its 10 LDS values once (8 rows +
+// halo), stores the shifted RDS rows (coalesced), takes the vertical 3-max in registers and the horizontal one
+// from neighbouring lanes (LDS only for the wave-edge columns), and ballots the peaks: no power tile in LDS and
+// no 9-read window per cell.  Same decisions as the general body (max is separable: 3x3 max = max of the
+// column-wise 3-max over j-1, j, j+1; 'reflect' edges repeat the in-window cell).
+template <int C, int KB, int NT>
+constexpr bool dd_reg_ok() {
+  return C % 64 == 0 && KB % 8 == 0 && (C / 64) * (KB / 8) * 64 == NT;
+}
+
+template <int C, int KB, int NT, int DBG = 0>
+RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
+                                 float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
+                                 int* __restrict__ row_count, float* __restrict__ dbmap,
+                                 float* __restrict__ pk_pow) {
+  constexpr int LD = lp_row(C) | 1;
+  constexpr int NCH = C / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = wave % NCH, rh = wave / NCH;
+  const int j = ch * 64 + lane;  // shifted Doppler column: out[j] = X[(j - C//2) mod C]
+  int d = j - C / 2;
+  if (d < 0) d += C;
+  int i0 = k0 + S / 2;  // shifted range row of LDS row 1
+  if (i0 >= S) i0 -= S;
+  const int rb = rh * 8;  // LDS rows rb .. rb + 9; interior rows rb + 1 .. rb + 8
+  float p[10];
+  const float2* col = buf + lp(d);
+  float2* dst = rds + ((size_t)fa * S + i0 + rb) * C + j;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const float2 z = col[(rb + r) * LD];
+    p[r] = cabs2(z);
+    if (r >= 1 && r <= 8) dst[(size_t)(r - 1) * C] = z;
+  }
+  float vm[8];
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr) {
+    const int i = i0 + rb + rr;
+    float m = p[rr + 1];
+    if (i > 0) m = fmaxf(m, p[rr]);          // 'reflect' at the shifted range edges: no neighbour
+    if (i + 1 < S) m = fmaxf(m, p[rr + 2]);
+    vm[rr] = m;
+  }
+  // wave-edge columns for the horizontal neighbours: xch[(rh * 8 + rr) * 2 NCH + 2 ch + {0: lane 0, 1: lane 63}]
+  float* ex = xch + (rb + 0) * 2 * NCH;
+  if (lane == 0 || lane == 63) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) ex[rr * 2 * NCH + 2 * ch + (lane == 63)] = vm[rr];
+  }
+  __syncthreads();
+  unsigned long long* wb = reinterpret_cast<unsigned long long*>(xch + KB * 2 * NCH);  // [KB][NCH] ballots
+  bool pkv[8];
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr) {
+    float l = __shfl_up(vm[rr], 1), r = __shfl_down(vm[rr], 1);
+    if (lane == 0) l = ch > 0 ? ex[rr * 2 * NCH + 2 * (ch - 1) + 1] : vm[rr];
+    if (lane == 63) r = ch + 1 < NCH ? ex[rr * 2 * NCH + 2 * (ch + 1)] : vm[rr];
+    const float m = fmaxf(fmaxf(l, vm[rr]), r);
+    const int i = i0 + rb + rr;
+    const float pc = p[rr + 1];
+    const bool pk = (i >= i_lo && i <= i_hi) && (pc > thr_f) && (pc >= m);
+    pkv[rr] = pk;
+    const unsigned long long b = __ballot(pk);
+    if (lane == 0) wb[(rb + rr) * NCH + ch] = b;
+    if (dbmap) dbmap[((size_t)fa * S + i) * C + j] = 10.f * log10f(pc + 1e-12f);
+  }
+  __syncthreads();
+  // peak powers compact over the tile's KB rows (one contiguous run from the tile's first row slot): the peaks
+  // of the rows before this wave's first row, then row by row
+  int pre = 0;
+  for (int x = 0; x < rb * NCH; ++x) pre += __popcll(wb[x]);
+  float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr) {
+    const int i = i0 + rb + rr;
+    const size_t row = (size_t)fa * S + i;
+    int off = pre, cnt = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int pc = __popcll(wb[(rb + rr) * NCH + c]);
+      off += c < ch ? pc : 0;
+      cnt += pc;
+    }
+    pre += cnt;
+    const unsigned long long b = wb[(rb + rr) * NCH + ch];
+    if (DBG != 5 && lane == 0) {  // DBG 5: no mask / count stores (ablation)
+      mask[row * NCH + ch] = b;
+      if (ch == 0) row_count[row] = cnt;
+    }
+    if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(b & ((1ull << lane) - 1ull))] = p[rr + 1];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2+K3 fused: Doppler FFT, fftshift, RDS store AND peak detection (dechirp.py:208-271) in one pass.
 // The block FFTs KB interior range bins plus one halo bin on each side (KB+2 rows), writes the KB shifted
@@ -236,8 +402,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
                                                              float* __restrict__ pk_pow, int xcd) {
   constexpr int NR = KB + 2;
   constexpr int LD = lp_rowp<PAD>(C) | 1;  // odd: conflict-free transposed (column) writes
-  constexpr int W = (C + 63) / 64;
-  constexpr int PER = (NR * C + NT - 1) / NT;
+    constexpr int PER = (NR * C + NT - 1) / NT;
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + C;
@@ -316,65 +481,85 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
     }
   }
   __syncthreads();
-  if constexpr (DBG != 1) fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);  // DBG 1: no FFT (ablation)
-  const int hs = S / 2, hc = C / 2;
-  int i0 = k0 + hs;  // shifted row of LDS row 1
-  if (i0 >= S) i0 -= S;
-  float2* dst = rds + ((size_t)fa * S + i0) * C;
-  // one pass over the tile: shifted RDS stores (interior rows) and |X|^2 kept in registers
-  float pr[PER];
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * NT;
-    pr[q] = 0.f;
-    if (idx < NR * C) {
-      const int r = idx / C, j = idx - r * C;  // j: shifted doppler index
-      int d = j - hc;                          // out[j] = X[(j - C//2) mod C]
-      if (d < 0) d += C;
-      const float2 z = buf[r * LD + lpp<PAD>(d)];
-      if (DBG != 2 && r >= 1 && r <= KB) dst[(size_t)(r - 1) * C + j] = z;  // DBG 2: no RDS store
-      pr[q] = cabs2(z);
-    }
+  if constexpr (PAD && (DBG == 0 || DBG >= 4) && dd_reg_ok<C, KB, NT>()) {
+    fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);
+    dd_tile_compute_reg<C, KB, NT, DBG>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi,
+                                   mask, row_count, dbmap, pk_pow);
+  } else {
+    dd_tile_compute<C, KB, NT, PAD, DBG>(buf, tws, S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap,
+                                         pk_pow);
   }
-  __syncthreads();
-  float* pw = reinterpret_cast<float*>(buf);  // power tile [NR][C], shifted doppler order
+}
+
+// Persistent K2+K3: the grid holds only resident workgroups.  Each XCD walks a contiguous range of tiles
+// (workgroup b serves XCD b % 8, tiles slot, slot + nb8, ... of that range: neighbouring tiles, whose halo rows
+// share cache lines, run back to back in one L2), and every workgroup issues the next tile's global loads into
+// registers right after staging the current tile in LDS, so HBM latency overlaps the FFT / store / detect phases.
+template <int C, int KB, int NT>
+__global__ __launch_bounds__(NT) void k_doppler_detect_p(const float2* __restrict__ work, int S,
+                                                         const float2* __restrict__ tw, float2* __restrict__ rds,
+                                                         float thr_f, int i_lo, int i_hi,
+                                                         unsigned long long* __restrict__ mask,
+                                                         int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                         float* __restrict__ pk_pow, long ntile) {
+  constexpr int NR = KB + 2;
+  constexpr int LD = lp_row(C) | 1;
+  constexpr int CS = NT / KB;
+  static_assert((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16),
+                "structured tile map required");
+  constexpr int PI = C / CS, PH = (2 * C + NT - 1) / NT;
+  extern __shared__ float2 sm[];
+  float2* tws = sm;
+  float2* buf = sm + C;
+  const int tid = threadIdx.x;
+  const int ri = tid % KB, cs = tid / KB;
+  for (int k = tid; k < C; k += NT) tws[k] = tw[k];
+  const unsigned nkb = (unsigned)(S / KB);
+  const long nb8 = gridDim.x >> 3;  // grid is a multiple of 8
+  const long x = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const long per = (ntile + 7) >> 3;
+  const long lo = x * per, hi = min(ntile, lo + per);
+  float2 ld[PI + PH];
+  auto issue = [&](long tile) {
+    const int kb = (int)((unsigned)tile % nkb);
+    const unsigned fa = (unsigned)tile / nkb;
+    const int k0 = kb * KB;
+    const float2* src = work + (size_t)fa * C * S;
+    const float2* p = src + (unsigned)(cs * S + k0 + ri);
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int idx = tid + q * NT;
-    if (idx < NR * C) pw[idx] = pr[q];
-  }
-  __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6;
-  for (int kk = wave; kk < (DBG == 3 ? 0 : KB); kk += NT / 64) {  // DBG 3: no detection
-    const int i = i0 + kk;
-    const bool gate = (i >= i_lo && i <= i_hi);
-    const bool has_up = i > 0, has_dn = i + 1 < S;
-    const float* up = pw + kk * C;
-    const float* mid = up + C;
-    const float* dn = mid + C;
-    const size_t row = (size_t)fa * S + i;
-    int cnt = 0;
+    for (int q = 0; q < PI; ++q) ld[q] = p[(unsigned)(q * CS * S)];
+    int kl = k0 - 1, kh = k0 + KB;
+    if (kl < 0) kl += S;
+    if (kh >= S) kh -= S;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const int j = w * 64 + lane;
-      bool pk = false;
-      float p = 0.f;
-      if (j < C) {
-        // 3x3 window max with 'reflect' edges (an out-of-range neighbour repeats an in-window cell)
-        const int jl = j > 0 ? j - 1 : j, jr = j + 1 < C ? j + 1 : j;
-        p = mid[j];
-        float m = fmaxf(fmaxf(mid[jl], p), mid[jr]);
-        if (has_up) m = fmaxf(m, fmaxf(fmaxf(up[jl], up[j]), up[jr]));
-        if (has_dn) m = fmaxf(m, fmaxf(fmaxf(dn[jl], dn[j]), dn[jr]));
-        pk = gate && (p > thr_f) && (p >= m);
-        if (dbmap) dbmap[row * C + j] = 10.f * log10f(p + 1e-12f);
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        ld[PI + h] = src[(unsigned)(c * S + (side ? kh : kl))];
       }
-      const unsigned long long b = __ballot(pk);
-      if (lane == 0) mask[row * W + w] = b;
-      if (pk_pow && pk) pk_pow[row * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = p;
-      cnt += __popcll(b);
     }
-    if (lane == 0) row_count[row] = cnt;
+  };
+  long t = lo + slot;
+  if (t < hi) issue(t);
+  for (; t < hi; t += nb8) {
+    float2* row = buf + (ri + 1) * LD + lp(cs);
+#pragma unroll
+    for (int q = 0; q < PI; ++q) row[lp(q * CS)] = ld[q];
+#pragma unroll
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        buf[(side ? NR - 1 : 0) * LD + lp(c)] = ld[PI + h];
+      }
+    }
+    __syncthreads();
+    if (t + nb8 < hi) issue(t + nb8);  // in flight during this tile's FFT, stores and detection
+    const int kb = (int)((unsigned)t % nkb);
+    dd_tile_compute<C, KB, NT, true, 0>(buf, tws, S, kb * KB, (unsigned)t / nkb, rds, thr_f, i_lo, i_hi, mask,
+                                        row_count, dbmap, pk_pow);
+    __syncthreads();  // the detection reads the LDS tile; the next tile's staging overwrites it
   }
 }
 
@@ -387,13 +572,15 @@ static int dd_xcd() {
 template <int C, int KB>
 static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw,
                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                int* row_count, float* dbmap, float* pk_pow) {
+                                int* row_count, float* dbmap, float* pk_pow, int* pk_group) {
+  *pk_group = 1;  // row-compact, except the register tile body (tile-compact: KB rows)
   const long ntile = (long)F * A * (S / KB);
   // padded LDS rows; RSL_DD_PAD=0 selects plain rows (smaller tile: measured slower, 2.14 vs 1.98 ms per 1000
   // cfg2 frames, also with the registers capped for 8 resident workgroups per CU)
   const char* pe = getenv("RSL_DD_PAD");
   const bool pad = !pe || atoi(pe) != 0;
-  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * ((pad ? lp_row(C) : C) | 1));
+  // + the register body's exchange area (edge columns and ballots: 16 B per row per 64 columns)
+  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * ((pad ? lp_row(C) : C) | 1)) + (size_t)KB * (C / 64) * 16;
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
   // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
@@ -406,6 +593,25 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
     if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1>;
     if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2>;
     if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3>;
+    if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4>;
+    if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5>;
+  }
+  if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {
+    const char* ep = getenv("RSL_DD_PERSIST");
+    if (pad && ep && atoi(ep) != 0 && !getenv("RSL_DD_DBG")) {
+      auto pk = k_doppler_detect_p<C, KB, NT>;
+      long nblk = resident_grid(reinterpret_cast<const void*>(pk), lds, ntile) & ~7L;
+      if (nblk >= 8) {
+        hipLaunchKernelGGL(pk, dim3((unsigned)nblk), dim3(NT), lds, st, work, S, tw, rds, thr_f, i_lo, i_hi, mask,
+                           row_count, dbmap, pk_pow, ntile);
+        return hipGetLastError();
+      }
+    }
+  }
+  if (pad && dd_reg_ok<C, KB, NT>()) {
+    const char* ed = getenv("RSL_DD_DBG");
+    const int v = ed ? atoi(ed) : 0;
+    if (v == 0 || v >= 4) *pk_group = KB;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds, thr_f, i_lo, i_hi, mask,
                      row_count, dbmap, pk_pow, dd_xcd());
@@ -429,11 +635,12 @@ static int dd_kb(int C, int S) {
 template <int C>
 static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
                              double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
-                             float* pk_pow) {
+                             float* pk_pow, int* pk_group) {
   constexpr int K0 = rows_for(C);
   constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
   const int kb = dd_kb(C, S);
-#define K2D(KBV) return launch_k2d_kb<C, KBV>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow)
+#define K2D(KBV) \
+  return launch_k2d_kb<C, KBV>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group)
   if (kb == K1) K2D(K1);
   if constexpr (C == 128) {  // tuning variants (RSL_DD_KB)
     if (kb == 8) K2D(8);
@@ -573,13 +780,14 @@ bool doppler_detect_supported(int C, int S) {
 
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported) {
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group) {
+  *pk_group = 1;
   *supported = doppler_detect_supported(C, S);
   if (!*supported || F <= 0 || A <= 0) return hipSuccess;
   switch (C) {
 #define CASE(n) \
   case n:       \
-    return launch_k2d<n>(st, work, F, A, S, tw_C, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+    return launch_k2d<n>(st, work, F, A, S, tw_C, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group);
     CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
 #undef CASE
     default:

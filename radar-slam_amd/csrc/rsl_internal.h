@@ -20,7 +20,7 @@ bool doppler_detect_supported(int C, int S);
 float threshold_as_float(double thr);  // largest float t <= thr
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported);
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);
@@ -34,9 +34,10 @@ hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long lo
                        const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
                        int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
 
-// Emit from row-compact peak powers and union masks (no RDS read); W = ceil(C/64) must be a power of two <= 64.
+// Emit from group-compact peak powers (pk_group rows per group, 1 = row-compact) and union masks (no RDS read);
+// W = ceil(C/64) must be a power of two <= 64.
 hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
-                        const float* pk_pow, int F, int A, int S, int C, const int* entry_row_off,
+                        const float* pk_pow, int pk_group, int F, int A, int S, int C, const int* entry_row_off,
                         const int* cell_row_off, const long long* entry_base, const long long* cell_base,
                         long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
                         double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);

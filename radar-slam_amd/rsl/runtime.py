@@ -110,14 +110,17 @@ class Context:
     def rds_detect(self, cube, table, thr_power: float, i_lo: int, i_hi: int, *, rds, work, mask, row_count,
                    peak_pow=None, db_map=None, chirp0: int = 0, num_chirps: Optional[int] = None,
                    dc_removal: bool = True):
-        """cube [F, A, Ct, S] -> rds [F, A, S, C] + detection outputs, Doppler FFT and detection in one kernel."""
+        """cube [F, A, Ct, S] -> rds [F, A, S, C] + detection outputs, Doppler FFT and detection in one kernel.
+        Returns the row grouping of ``peak_pow`` (pass it to ``emit``)."""
         F, A, Ct, S = cube.shape
         C = Ct - chirp0 if num_chirps is None else num_chirps
+        group = ctypes.c_int(1)
         self._bind()
         self.check(self.lib.rsl_rds_detect(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table), int(dc_removal),
                                            _ptr(work), _ptr(rds), float(thr_power), int(i_lo), int(i_hi), _ptr(mask),
-                                           _ptr(row_count), _ptr(db_map), _ptr(peak_pow)), 'rsl_rds_detect')
-        return rds
+                                           _ptr(row_count), _ptr(db_map), _ptr(peak_pow), ctypes.byref(group)),
+                   'rsl_rds_detect')
+        return int(group.value)
 
     # -- a8 -------------------------------------------------------------------------------------
     def detect(self, rds, thr_power: float, i_lo: int, i_hi: int, want_db: bool = False, out=None):
@@ -157,9 +160,9 @@ class Context:
                     union_mask=um)
 
     def emit(self, rds, mask, offs, entry_cap: int, cell_cap: int, want_pdb: bool = True, bufs=None,
-             peak_pow=None):
-        """Compact peak entries and unique cells.  With ``peak_pow`` (from detect) and the offsets' union mask the
-        RDS is not re-read."""
+             peak_pow=None, peak_pow_group: int = 1):
+        """Compact peak entries and unique cells.  With ``peak_pow`` (from detect, row grouping 1; or rds_detect,
+        the grouping it returned) and the offsets' union mask the RDS is not re-read."""
         torch = self.torch
         F, A, S, C = rds.shape
         b = bufs or {}
@@ -174,7 +177,8 @@ class Context:
                            get('c_amask', cell_cap, torch.int32))
         self._bind()
         self.check(self.lib.rsl_peak_emit(self.h, _ptr(rds), _ptr(mask), _ptr(offs.get('union_mask')),
-                                          _ptr(peak_pow), F, A, S, C, _ptr(offs['entry_row_off']),
+                                          _ptr(peak_pow), int(peak_pow_group), F, A, S, C,
+                                          _ptr(offs['entry_row_off']),
                                           _ptr(offs['cell_row_off']), _ptr(offs['entry_base']),
                                           _ptr(offs['cell_base']), int(entry_cap), int(cell_cap), _ptr(e_ant),
                                           _ptr(e_r), _ptr(e_d), _ptr(e_c), _ptr(e_pdb), _ptr(c_f), _ptr(c_rc),
