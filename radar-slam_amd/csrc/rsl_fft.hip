@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // and issues the next tile's 16-B global loads into registers before running the current tile's LDS FFT, so
 // HBM latency overlaps the FFT instead of stalling every tile's load phase.  Requires even S with
 // rows_for(S) * S / 2 a multiple of the block size (every power-of-two S >= 16).
-template <int S, int CB>
+template <int S, int CB, int DBG = 0>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
     }
     __syncthreads();
     if (t + gridDim.x < ntile) load(t + gridDim.x);  // in flight during the FFT below
-    fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);
+    if constexpr (DBG != 1) fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);  // DBG 1: no FFT (ablation)
     if (dc) {
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
       __syncthreads();
@@ -659,9 +659,12 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       constexpr int CBX = decltype(cbc)::value;
       const long ntile = (long)F * A * ((C + CBX - 1) / CBX);
       const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CBX * lp_row(S));
-      const long nblk = resident_grid(reinterpret_cast<const void*>(k_range_fft_p<S, CBX>), lds, ntile);
-      hipLaunchKernelGGL((k_range_fft_p<S, CBX>), dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C,
-                         ntile, table, tw, dc, work);
+      auto kern = k_range_fft_p<S, CBX>;
+      if (const char* e = getenv("RSL_RF_DBG"))  // ablation (timing only: results are wrong)
+        if (atoi(e) == 1) kern = k_range_fft_p<S, CBX, 1>;
+      const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile, table, tw,
+                         dc, work);
       return hipGetLastError();
     };
     if constexpr (S == 512) {  // RSL_RF_CB: chirp rows per tile (4 / 8 / 16) for tuning
