@@ -43,42 +43,18 @@ def pmc_traffic(kernel_prefix, frames_per_launch):
         if name.startswith('rsl::' + kernel_prefix) and 'hbm_bytes' in e:
             return e['hbm_bytes'] * frames_per_launch / prof.get('frames_per_launch', 1000)
     return None
-SCENE = [  # tests/test_synth_raw.py:165-190 (reference)
-    (20.0, 0.0, -10.0, 0.0), (40.0, math.radians(45.0), -8.0, 5.0), (60.0, math.radians(-30.0), -12.0, -3.0)]
+SCENE = [  # tests/test_synth_raw.py:165-190 (reference): range m, azimuth rad, rcs dBsm, radial velocity m/s
+    dict(range_sc=20.0, azimuth_sc=0.0, rcs=-10.0, vr=0.0),
+    dict(range_sc=40.0, azimuth_sc=math.radians(45.0), rcs=-8.0, vr=5.0),
+    dict(range_sc=60.0, azimuth_sc=math.radians(-30.0), rcs=-12.0, vr=-3.0)]
 
 
-def target_pattern(A, S, fc=77e9, B=1e9, Tc=51.2e-6):
-    """Noise-free scatterer response [A, S] of simulate_raw.synthesize_frame (simulate_raw.py:102-209):
-    independent of the chirp index, so one pattern serves every chirp of every frame."""
-    c = 3e8
-    lam = c / fc
-    pos = np.arange(A) * lam / 2
-    t = np.linspace(0, Tc, S)
-    k = B / Tc
-    chirp = lambda tt: np.exp(1j * 2 * np.pi * (fc * tt + 0.5 * k * tt ** 2))
-    ref = chirp(t)
-    out = np.zeros((A, S), complex)
-    for r, az, rcs, vr in SCENE:
-        amp = np.sqrt(10 ** (rcs / 10)) / (4 * np.pi * r ** 2)
-        ph = amp * np.exp(1j * (4 * np.pi * vr * fc / c + 2 * np.pi * pos * np.sin(az) / lam))
-        td = t - 2 * r / c
-        v = (td >= 0) & (td <= Tc)
-        out[:, v] += ph[:, None] * (chirp(td[v]) * np.conj(ref[v]))[None, :]
-    return out
-
-
-def make_cubes(torch, dev, nb, F, A, C, S, seed):
-    pat = torch.from_numpy(target_pattern(A, S).astype(np.complex64)).to(dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    cubes = []
-    sig = math.sqrt(0.01)  # noise_power 0.01 (simulate_raw.py:216-218)
-    for _ in range(nb):
-        x = torch.randn((F, A, C, S, 2), device=dev, generator=g, dtype=torch.float32).mul_(sig)
-        z = torch.view_as_complex(x)
-        z += pat[None, :, None, :]
-        cubes.append(z)
-    return cubes
+def make_cubes(ctx, nb, F, A, C, Tc, rank):
+    """nb batches of F synthetic frames from the device generator (rsl_synth_*: the reference simulator's scene
+    model, simulate_raw.py:102-221, plus Philox complex Gaussian noise of power 0.01); frame blocks differ by rank."""
+    import rsl
+    gen = rsl.SyntheticCubes(ctx, SCENE, chirp_duration=Tc, num_chirps=C, num_antennas=A, noise_power=0.01)
+    return [gen.generate(F, seed=1234, frame0=(rank * nb + i) * F) for i in range(nb)]
 
 
 def cpu_baseline(budget_s=20.0):
@@ -165,7 +141,7 @@ def main():
     chain = chains[0]
     streams = [torch.cuda.Stream(dev) for _ in range(NS)]
     nb = 2
-    cubes = make_cubes(torch, dev, nb, F, A, C, S, seed=1234 + 7919 * rank)
+    cubes = make_cubes(ctx, nb, F, A, C, cfg.chirp_duration, rank)
     # trajectory reduction: device prefix scan of this rank's frame block, all-gather of the
     # 16-double block summaries and of the per-frame poses over RCCL/xGMI (rsl/traj.py)
     reducer = rsl.TrajectoryReducer(ctx, F, dt=cfg.dt)

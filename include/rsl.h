@@ -219,6 +219,18 @@ int rsl_traj_stitch(rsl_handle h, const void* summaries, int R, int rank, double
 /* uniform_filter1d(x[:, c], size, mode='nearest') per column (pose_integration.py:105-109); x, out f64 [F][ncol]. */
 int rsl_traj_smooth(rsl_handle h, const void* x, long long F, int ncol, int size, void* out);
 
+/* SURVEY §8f #2  FMCWRadarSimulator.synthesize_frame (scripts/simulate_raw.py:147-221) at batch scale.
+ *     rsl_synth_pattern: the deterministic part, which does not depend on the chirp index, as fp64 complex
+ *       pattern [A][S] (device) from scatterers f64 [n][4] = {range m, azimuth rad, rcs dBsm, radial velocity m/s}
+ *       (device); antenna_spacing <= 0 means lambda / 2; S = samples per chirp (int(chirp_duration * fs)).
+ *     rsl_synth_cube: cube c64 [F][A][C][S] = pattern + sqrt(noise_power) (n1 + j n2) with standard normal n1, n2
+ *       from Philox-4x32-10 (key = seed, counter = global sample index / 2 counted from frame frame0) and
+ *       Box-Muller; S must be even.  Frame blocks generated separately (e.g. one per rank) equal one large call. */
+int rsl_synth_pattern(rsl_handle h, const void* scatterers, int n, int A, int S, double fc, double bandwidth,
+                      double chirp_duration, double antenna_spacing, void* pattern);
+int rsl_synth_cube(rsl_handle h, const void* pattern, int F, int A, int C, int S, double noise_power,
+                   unsigned long long seed, long long frame0, void* cube);
+
 #ifdef __cplusplus
 }
 #endif

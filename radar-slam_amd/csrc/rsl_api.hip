@@ -585,3 +585,31 @@ int rsl_traj_stitch(rsl_handle h, const void* summaries, int R, int rank, double
                                            (double*)base),
                    "traj_stitch");
 }
+
+int rsl_synth_pattern(rsl_handle h, const void* scatterers, int n, int A, int S, double fc, double bandwidth,
+                      double chirp_duration, double antenna_spacing, void* pattern) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 0 || A <= 0 || S <= 0 || !(fc > 0) || !(chirp_duration > 0))
+    return fail(h, RSL_ERR_INVALID, "rsl_synth_pattern: bad arguments");
+  if (!pattern || (n > 0 && !scatterers)) return fail(h, RSL_ERR_INVALID, "rsl_synth_pattern: null pointer");
+  const double d = antenna_spacing > 0 ? antenna_spacing : 0.5 * 3e8 / fc;
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_synth_pattern(h->stream, (const double*)scatterers, n, A, S, fc, bandwidth,
+                                             chirp_duration, d, (double2*)pattern),
+                   "synth_pattern");
+}
+
+int rsl_synth_cube(rsl_handle h, const void* pattern, int F, int A, int C, int S, double noise_power,
+                   unsigned long long seed, long long frame0, void* cube) {
+  if (!h) return RSL_ERR_INVALID;
+  if (F < 0 || A <= 0 || C <= 0 || S <= 0 || frame0 < 0 || !(noise_power >= 0))
+    return fail(h, RSL_ERR_INVALID, "rsl_synth_cube: bad arguments");
+  if (S % 2) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_synth_cube: S must be even");
+  if (!pattern || !cube) return fail(h, RSL_ERR_INVALID, "rsl_synth_cube: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_synth_cube(h->stream, (const double2*)pattern, F, A, C, S, noise_power, seed, frame0,
+                                          (float2*)cube),
+                   "synth_cube");
+}

@@ -94,4 +94,10 @@ hipError_t launch_phase_model(hipStream_t st, const double* pos, const double* a
                               const double* y, int wrap, double ridge, double* pred, double* resid, double* cost);
 hipError_t launch_bvls(hipStream_t st, const double* pos, const double* ang, long n, const double* y, double k, int nv,
                        double ridge, const double* lo, const double* hi, double* out);
+// Synthetic cube generator (simulate_raw.py:102-221): fp64 [A, S] pattern, then pattern + Philox noise.
+hipError_t launch_synth_pattern(hipStream_t st, const double* sc, int n, int A, int S, double fc, double bandwidth,
+                                double Tc, double d, double2* pattern);
+hipError_t launch_synth_cube(hipStream_t st, const double2* pattern, int F, int A, int C, int S, double noise_power,
+                             unsigned long long seed, long long frame0, float2* cube);
+
 }  // namespace rsl

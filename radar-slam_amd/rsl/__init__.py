@@ -10,6 +10,8 @@ from ._lib import LIB_PATH, load  # noqa: F401
 from .runtime import Context, get_context  # noqa: F401
 from .chain import ChainConfig, RadarChain  # noqa: F401
 from .traj import TrajectoryReducer  # noqa: F401
+from .synth import SyntheticCubes  # noqa: F401
 from . import tables  # noqa: F401
 
-__all__ = ['Context', 'get_context', 'ChainConfig', 'RadarChain', 'TrajectoryReducer', 'tables', 'load', 'LIB_PATH']
+__all__ = ['Context', 'get_context', 'ChainConfig', 'RadarChain', 'TrajectoryReducer', 'SyntheticCubes', 'tables', 'load',
+           'LIB_PATH']

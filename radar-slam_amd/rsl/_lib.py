@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import c_double, c_float, c_int, c_longlong, c_void_p, c_char_p, POINTER
+from ctypes import c_double, c_float, c_int, c_longlong, c_ulonglong, c_void_p, c_char_p, POINTER
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get('RSL_LIBRARY', os.path.join(PKG_ROOT, 'lib', 'librsl.so'))
@@ -62,6 +62,8 @@ SIGNATURES = {
     'rsl_traj_apply': (c_int, [_P, _P, _P, c_longlong, _P]),
     'rsl_traj_stitch': (c_int, [_P, _P, c_int, c_int, c_double, c_int, _P, _P]),
     'rsl_traj_smooth': (c_int, [_P, _P, c_longlong, c_int, c_int, _P]),
+    'rsl_synth_pattern': (c_int, [_P, _P, c_int, c_int, c_int, c_double, c_double, c_double, c_double, _P]),
+    'rsl_synth_cube': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_ulonglong, c_longlong, _P]),
     'rsl_bvls': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, _P, _P, _P]),
 }
 
