@@ -90,10 +90,14 @@ __global__ __launch_bounds__(256) void k_synth_cube(const double2* __restrict__ 
     const int s = (int)(g % S);
     const int a = (int)((g / cs) % A);
     const double2 q0 = pattern[(size_t)a * S + s], q1 = pattern[(size_t)a * S + s + 1];
-    float s0, c0, s1, c1;
-    const float r0 = sigma * sqrtf(-2.0f * logf(u01(x.x))), r1 = sigma * sqrtf(-2.0f * logf(u01(x.z)));
-    sincospif(2.0f * u01(x.y), &s0, &c0);
-    sincospif(2.0f * u01(x.w), &s1, &c1);
+    // Box-Muller on the hardware transcendentals: v_log_f32 is log2, v_sin/v_cos_f32 take revolutions
+    // (sin(2 pi u) in one instruction); ~1e-6 absolute on unit normals, far below the noise's own scale
+    constexpr float kM2Ln2 = -1.38629436111989061883f;  // -2 ln 2
+    const float r0 = sigma * __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(x.x)));
+    const float r1 = sigma * __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(x.z)));
+    const float u1 = u01(x.y), u3 = u01(x.w);
+    const float s0 = __builtin_amdgcn_sinf(u1), c0 = __builtin_amdgcn_cosf(u1);
+    const float s1 = __builtin_amdgcn_sinf(u3), c1 = __builtin_amdgcn_cosf(u3);
     cube[p] = make_float4((float)q0.x + r0 * c0, (float)q0.y + r0 * s0, (float)q1.x + r1 * c1,
                           (float)q1.y + r1 * s1);
   }
