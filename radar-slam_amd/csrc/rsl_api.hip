@@ -225,6 +225,21 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   bool sup = true;
   int group = 1;
   hipError_t e;
+  if (!db_map && rsl::rds_fused_supported(C, S)) {  // one pass over the cube; `work` holds the Doppler 3-max
+    {
+      Scope sc(h, RSL_K_RANGE_FFT);
+      e = rsl::launch_rds_fused(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
+                                tC, dc_removal, (float2*)rds, work, thr_power, i_lo, i_hi);
+    }
+    if (int r = hip_check(h, e, "rds_fused")) return r;
+    {
+      Scope sc(h, RSL_K_DOPPLER_FFT);
+      e = rsl::launch_detect_finish(h->stream, work, F, A, C, S, (unsigned long long*)mask, (int*)row_count,
+                                    (float*)peak_pow, &group);
+    }
+    if (peak_pow_group) *peak_pow_group = group;
+    return hip_check(h, e, "detect_finish");
+  }
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,

@@ -109,6 +109,16 @@ RSL_DEV float tile_max(const floatx16& a) {
   return __int_as_float(mx3(mx3(m0, m1, m2), mx3(m3, m4, v[15]), INT_MIN));
 }
 
+// Record-tile copy for the lanes that set a new record: 8 v_pk_mov_b32 (64-bit pairs) under the branch's exec mask
+// instead of 16 v_cndmask_b32 on every tile.  Volatile asm also keeps the compiler from speculating the branch into
+// per-value selects.
+RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
+  typedef double doublex8 __attribute__((ext_vector_type(8)));
+  const doublex8 s = __builtin_bit_cast(doublex8, src);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,1]" : "=v"(dst[k]) : "v"(s[k]));
+}
+
 // Exact fp64 scan of one cell (MUSIC near-degenerate path): key = P if M - P > 1e-12 else -1, first index.
 template <int MA>
 RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __restrict__ steer64, int& idx,
@@ -151,8 +161,8 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
 // column n), so each lane computes the Toeplitz column of its own cell once and swaps the other K half with
 // lane l ^ 32 (no redundant loads or autocorrelations), and the fused ESPRIT / phase work of a pass is spread
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
-template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0>
-__global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : 1))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
@@ -257,13 +267,12 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
     // replicate row G-1 and so never win.
     float best0 = -INFINITY, best1 = -INFINITY;
     int bt0 = 0, bt1 = 0;
-    float sv0[16], sv1[16];
+    double sv0[8], sv1[8];  // record tiles as 64-bit register pairs (copied with v_pk_mov_b32)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      sv0[i] = 0.f;
-      sv1[i] = 0.f;
-    }
-    for (int t = 0; t < ntiles; ++t) {
+    for (int k = 0; k < 8; ++k) sv0[k] = sv1[k] = 0.0;
+    const int ntl = NTC ? NTC : ntiles;  // NTC: compile-time tile count (fully unrolled loop)
+#pragma unroll
+    for (int t = 0; t < ntl; ++t) {
       floatx16 acc0 = {}, acc1 = {};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
@@ -286,32 +295,28 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x1h, acc1, 0, 0, 0);
         }
       }
-      {
-        const float m = tile_max(acc0);
-        const bool u = m > best0;
-        best0 = u ? m : best0;
-        bt0 = u ? t : bt0;
-        if constexpr (DBG != 1) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sv0[i] = u ? acc0[i] : sv0[i];
-        }
+      // record tiles: a real branch (exec-masked 64-bit register copies for the lanes that set a record) instead of
+      // a v_cndmask per value
+      const float m0 = tile_max(acc0), m1 = tile_max(acc1);
+      if (m0 > best0) {
+        best0 = m0;
+        bt0 = t;
+        if constexpr (DBG != 1) copy_tile(sv0, acc0);
       }
-      {
-        const float m = tile_max(acc1);
-        const bool u = m > best1;
-        best1 = u ? m : best1;
-        bt1 = u ? t : bt1;
-        if constexpr (DBG != 1) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sv1[i] = u ? acc1[i] : sv1[i];
-        }
+      if (m1 > best1) {
+        best1 = m1;
+        bt1 = t;
+        if constexpr (DBG != 1) copy_tile(sv1, acc1);
       }
     }
     int i0 = 15, i1 = 15;
+    {
+      const floatx16 r0 = __builtin_bit_cast(floatx16, sv0), r1 = __builtin_bit_cast(floatx16, sv1);
 #pragma unroll
-    for (int i = 14; i >= 0; --i) {
-      i0 = (sv0[i] == best0) ? i : i0;
-      i1 = (sv1[i] == best1) ? i : i1;
+      for (int i = 14; i >= 0; --i) {
+        i0 = (r0[i] == best0) ? i : i0;
+        i1 = (r1[i] == best1) ? i : i1;
+      }
     }
     int g0 = 32 * bt0 + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
     int g1 = 32 * bt1 + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
@@ -331,7 +336,11 @@ __global__ __launch_bounds__(256) void k_doa_toep(const float2* __restrict__ rds
     if (bidx >= G) bidx = G - 1;
     float gval = best * (1.0f / kToepScale);
     if constexpr (MUSIC) {
-      if (best >= mthr && c < ncell) exact_scan<MA>(s, A, G, steer64, bidx, gval);  // rare
+      if (best >= mthr && c < ncell) {  // rare: reload the signature (keeps s dead across the tile loop)
+        float2 sr[MA];
+        load_sig_c<MA>(rds, cfr, crc, c, true, A, plane, fstride, sr);
+        exact_scan<MA>(sr, A, G, steer64, bidx, gval);
+      }
     }
     if (c < ncell) {
       out_idx[c] = bidx;
@@ -346,6 +355,10 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
                                 int ntiles, int G, const double* steer64, int* out_idx, float* out_gmax,
                                 double esprit_scale, double* out_esprit, double* out_phase, int max_blocks) {
   auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS>;
+  if constexpr (MA == 8) {  // the 0.5-degree grid (G = 361: 12 tiles of 32): unrolled tile loop
+    const char* eu = getenv("RSL_DOA_UNROLL");
+    if (ntiles == 12 && (!eu || atoi(eu) != 0)) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12>;
+  }
   if constexpr (MUSIC && !GMAX && !EXTRAS && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing studies only)
     if (const char* e = getenv("RSL_DOA_DBG")) {
       const int v = atoi(e);

@@ -21,6 +21,15 @@ float threshold_as_float(double thr);  // largest float t <= thr
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
                                  int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group);
+// K12 + K3' (rsl_rds_fused.hip): one-pass range + Doppler FFT per (slab, range class) with the Doppler-direction half
+// of detection (Doppler 3-max + candidate bits into `work`), then the range-direction finish -> the same mask /
+// row_count / tile-compact peak powers as launch_doppler_detect.  S = 512, C = 128; opt-in with RSL_FUSED=1 (slower).
+bool rds_fused_supported(int C, int S);
+hipError_t launch_rds_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
+                            const float2* table, const float2* tw_S, const float2* tw_C, int dc, float2* rds,
+                            void* work, double thr_p, int i_lo, int i_hi);
+hipError_t launch_detect_finish(hipStream_t st, const void* work, int F, int A, int C, int S,
+                                unsigned long long* mask, int* row_count, float* pk_pow, int* pk_group);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);

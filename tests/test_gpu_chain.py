@@ -3,6 +3,8 @@
 Cubes come from the oracle's restatement of simulate_raw.synthesize_frame (bit-identical to the
 reference, pinned in test_oracle_golden.py) and are fed to the GPU as complex64.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -18,6 +20,7 @@ CFGS = {  # name: (A, C, T_c)
     'cfg2': (8, 128, 51.2e-6),
     'cfg5a16': (16, 32, 12.8e-6),
     'cfg5': (16, 256, 102.4e-6),  # configs[4] frame shape (A16 C256 S1024), one frame
+    'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
 }
 FRAMES = {'cfg5': 1}
 DOA_SAMPLE = 30000  # cells checked per frame against the oracle scan (random subset above this; cfg5 has ~207 K)
@@ -41,8 +44,13 @@ def runs(ctx):
         cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
         ch = rsl.RadarChain(cfg, F, ctx)
         cube = ctx.to_dev(frames.astype(np.complex64))
-        ch.run(cube)
-        res = ch.results()
+        if name.endswith('_onepass'):
+            os.environ['RSL_FUSED'] = '1'
+        try:
+            ch.run(cube)
+            res = ch.results()
+        finally:
+            os.environ.pop('RSL_FUSED', None)
         res['rds'] = ch.rds.cpu().numpy()
         res['mask_words'] = ch.mask.cpu().numpy()
         res['frames'] = frames
