@@ -123,9 +123,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if 'RSL_BENCH_DEVICE' in os.environ:  # rehearsal of the N > 1 path on a one-GPU box (all ranks on one device)
+        local = int(os.environ['RSL_BENCH_DEVICE'])
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        backend = os.environ.get('RSL_BENCH_BACKEND', 'nccl')  # nccl = RCCL over xGMI; gloo only for rehearsals
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
