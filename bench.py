@@ -116,6 +116,10 @@ def main():
     ap.add_argument('--no-timing', action='store_true', help='disable per-kernel hipEvent timing')
     ap.add_argument('--streams', type=int, default=int(os.environ.get('RSL_BENCH_STREAMS', '1')),
                     help='concurrent HIP streams per GPU; each runs the chain on F/streams frames of the step')
+    ap.add_argument('--pipeline', type=int, default=int(os.environ.get('RSL_BENCH_PIPELINE', '0')),
+                    help='1: double-buffered chains on two streams; batch i+1\'s memory-bound front half (RDS, '
+                         'detection, compaction) runs concurrently with batch i\'s compute-bound back half (DoA, '
+                         'velocity, trajectory)')
     args = ap.parse_args()
 
     import torch
@@ -154,7 +158,35 @@ def main():
 
     main = torch.cuda.current_stream(dev)
 
+    if args.pipeline:
+        NS = 1
+        vel2 = torch.empty((2, F, 8), dtype=torch.float64, device=dev)
+        chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
+        chain = chains[0]
+        sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        evA = [torch.cuda.Event() for _ in range(2)]
+        evB = [torch.cuda.Event() for _ in range(2)]
+        used = [False, False]
+
+    def step_pipelined(i):
+        k = i % 2
+        ch = chains[k]
+        sA.wait_stream(main)
+        with torch.cuda.stream(sA):
+            if used[k]:
+                sA.wait_event(evB[k])  # batch i-2's back half is done with these buffers
+            ch.run_front(cubes[i % nb])
+            evA[k].record(sA)
+        with torch.cuda.stream(sB):
+            sB.wait_event(evA[k])
+            ch.run_back()
+            reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
+            evB[k].record(sB)
+        used[k] = True
+
     def step(i):
+        if args.pipeline:
+            return step_pipelined(i)
         cube = cubes[i % nb]
         for k, (ch, st) in enumerate(zip(chains, streams)):  # independent frame slices, concurrent streams
             st.wait_stream(main)
@@ -191,8 +223,9 @@ def main():
         elapsed = float(tt.item())
     kt = ctx.timing_read() if not args.no_timing else {}
     ctx.timing(False)
-    ne = sum(ch.totals()[0] for ch in chains)
-    nc = sum(ch.totals()[1] for ch in chains)
+    counted = chains[:1] if args.pipeline else chains  # pipelined: both buffers hold a full batch
+    ne = sum(ch.totals()[0] for ch in counted)
+    nc = sum(ch.totals()[1] for ch in counted)
     frames_total = F * args.steps * world
     fps = frames_total / elapsed
 
@@ -208,7 +241,8 @@ def main():
         "config": {"workload": "configs[2]: 8ch x 128chirp x 512 synthetic cube, full chain "
                                "(RDS + peaks + MUSIC argmax + ESPRIT + LS velocity + trajectory)",
                    "frames_per_step": F, "frames_per_gpu_per_step": F, "antennas": A, "chirps": C, "samples": S,
-                   "doa_grid": G, "streams_per_gpu": NS, "parallelism": f"frame-sharded x{world}"},
+                   "doa_grid": G, "streams_per_gpu": 2 if args.pipeline else NS,
+                   "pipelined": bool(args.pipeline), "parallelism": f"frame-sharded x{world}"},
         "peaks_per_frame": ne / F, "cells_per_frame": nc / F,
     }
     if kt:

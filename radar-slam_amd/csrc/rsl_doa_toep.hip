@@ -72,26 +72,35 @@ RSL_DEV void split8(const float* v, uint4& hi, uint4& lo) {
   lo = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-RSL_DEV uint4 shfl_xor32_u4(uint4 v) {
-  return make_uint4((unsigned)__shfl_xor((int)v.x, 32), (unsigned)__shfl_xor((int)v.y, 32),
-                    (unsigned)__shfl_xor((int)v.z, 32), (unsigned)__shfl_xor((int)v.w, 32));
-}
-
-RSL_DEV uint4 sel_u4(bool c, uint4 a, uint4 b) {
-  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+// v_permlane32_swap on each dword: the upper 32 lanes of a are exchanged with the lower 32 lanes of b.
+RSL_DEV void swap32_u4(uint4& a, uint4& b) {
+  unsigned av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(av[j], bv[j], false, false);
+    av[j] = r[0];
+    bv[j] = r[1];
+  }
+  a = make_uint4(av[0], av[1], av[2], av[3]);
+  b = make_uint4(bv[0], bv[1], bv[2], bv[3]);
 }
 
 template <int MA>
 RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
                         long long c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
-  // unconditional loads from always-valid addresses (antenna clamped to A-1, cell 0 when out of range),
-  // then a select: no per-antenna branches
+  // loads from always-valid addresses (cell 0 past the end: its results are never stored); antennas past A
+  // (A < MA, wave-uniform) are clamped to A-1 and zeroed
   const long long cc = ok ? c : 0;
   const float2* base = rds + (size_t)cfr[cc] * fstride + crc[cc];
+  if (A >= MA) {
 #pragma unroll
-  for (int m = 0; m < MA; ++m) {
-    const float2 z = base[(size_t)(m < A ? m : A - 1) * plane];
-    s[m] = (ok && m < A) ? z : make_float2(0.f, 0.f);
+    for (int m = 0; m < MA; ++m) s[m] = base[(size_t)m * plane];
+  } else {
+#pragma unroll
+    for (int m = 0; m < MA; ++m) {
+      const float2 z = base[(size_t)(m < A ? m : A - 1) * plane];
+      s[m] = m < A ? z : make_float2(0.f, 0.f);
+    }
   }
 }
 
@@ -247,18 +256,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        // both K halves split with static register indices, then selected by h (an index into e[] that
-        // depends on the lane becomes a compare/select chain per element)
+        // E0 / E1 = the own cell's K rows 16 kb .. +7 / +8 .. +15.  Column tile 0 (cells of lanes 0-31) needs
+        // [E0 of lanes 0-31 | E1 of lanes 0-31 moved up], column tile 1 [E0 of lanes 32-63 moved down | E1 of lanes
+        // 32-63]: exactly what v_permlane32_swap does to the pair (E0, E1), one instruction per dword
         uint4 h0h, h0l, h1h, h1l;
         split8(e + 16 * kb, h0h, h0l);
         split8(e + 16 * kb + 8, h1h, h1l);
-        const uint4 oh = sel_u4(h == 0, h0h, h1h), ol = sel_u4(h == 0, h0l, h1l);  // own cell, K rows 8h..8h+7
-        const uint4 xh = sel_u4(h == 0, h1h, h0h), xl = sel_u4(h == 0, h1l, h0l);  // own cell, partner's K half
-        const uint4 rh = shfl_xor32_u4(xh), rl = shfl_xor32_u4(xl);  // partner's cell, K rows 8h..8h+7
-        b0h[kb] = sel_u4(h == 0, oh, rh);
-        b0l[kb] = sel_u4(h == 0, ol, rl);
-        b1h[kb] = sel_u4(h == 0, rh, oh);
-        b1l[kb] = sel_u4(h == 0, rl, ol);
+        swap32_u4(h0h, h1h);
+        swap32_u4(h0l, h1l);
+        b0h[kb] = h0h;
+        b0l[kb] = h0l;
+        b1h[kb] = h1h;
+        b1l[kb] = h1l;
       }
     }
     // Argmax epilogue per column tile: the tile max (v_max3 tree), a strict '>' record test and a conditional
@@ -270,10 +279,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     double sv0[8], sv1[8];  // record tiles as 64-bit register pairs (copied with v_pk_mov_b32)
 #pragma unroll
     for (int k = 0; k < 8; ++k) sv0[k] = sv1[k] = 0.0;
-    const int ntl = NTC ? NTC : ntiles;  // NTC: compile-time tile count (fully unrolled loop)
-#pragma unroll
-    for (int t = 0; t < ntl; ++t) {
-      floatx16 acc0 = {}, acc1 = {};
+    auto mma = [&](int t, floatx16& acc0, floatx16& acc1) {
+      acc0 = floatx16{};
+      acc1 = floatx16{};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         const half8 ah = __builtin_bit_cast(half8, tt[(((t * KB + kb) * 2) + 0) * 64 + lane]);
@@ -295,8 +303,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, x1h, acc1, 0, 0, 0);
         }
       }
-      // record tiles: a real branch (exec-masked 64-bit register copies for the lanes that set a record) instead of
-      // a v_cndmask per value
+    };
+    // record tiles: a real branch (exec-masked 64-bit register copies for the lanes that set a record) instead of
+    // a v_cndmask per value
+    auto record = [&](int t, const floatx16& acc0, const floatx16& acc1) {
       const float m0 = tile_max(acc0), m1 = tile_max(acc1);
       if (m0 > best0) {
         best0 = m0;
@@ -307,6 +317,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         best1 = m1;
         bt1 = t;
         if constexpr (DBG != 1) copy_tile(sv1, acc1);
+      }
+    };
+    {
+      const int ntl = NTC ? NTC : ntiles;  // NTC: compile-time tile count (fully unrolled loop)
+#pragma unroll
+      for (int t = 0; t < ntl; ++t) {
+        floatx16 acc0, acc1;
+        mma(t, acc0, acc1);
+        record(t, acc0, acc1);
       }
     }
     int i0 = 15, i1 = 15;
@@ -372,6 +391,8 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   if (lds > 64 * 1024) return hipErrorInvalidValue;  // caller checks toep_table_fits()
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+  if (const char* e = getenv("RSL_DOA_BPC"))  // blocks-per-CU cap: leaves room for a concurrent kernel (pipelined chain)
+    if (atoi(e) > 0 && atoi(e) < nb) nb = atoi(e);
   int dev = 0, ncu = 256;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

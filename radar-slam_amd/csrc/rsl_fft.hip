@@ -21,6 +21,8 @@ static long resident_grid(const void* kern, size_t lds, long ntile) {
   int nb = 0, dev = 0, ncu = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kThreads, lds) != hipSuccess || nb < 1) nb = 1;
   if (nb > 8) nb = 8;
+  if (const char* e = getenv("RSL_RF_BPC"))  // blocks-per-CU cap (pipelined chain: room for a concurrent kernel)
+    if (atoi(e) > 0 && atoi(e) < nb) nb = atoi(e);
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const long g = (long)nb * ncu;
@@ -654,7 +656,9 @@ template <int S>
 static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
                             const float2* table, const float2* tw, int dc, float2* work) {
   constexpr int CB = rows_for(S);
+  const char* enp = getenv("RSL_RF_NP");  // 1: one tile per workgroup (interleaves with a concurrent kernel)
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
+    if (!(enp && atoi(enp) != 0)) {
     auto go = [&](auto cbc) -> hipError_t {
       constexpr int CBX = decltype(cbc)::value;
       const long ntile = (long)F * A * ((C + CBX - 1) / CBX);
@@ -674,6 +678,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       if (v == 16) return go(std::integral_constant<int, 16>{});
     }
     return go(std::integral_constant<int, CB>{});
+    }
   }
   const long nblk = (long)F * A * ((C + CB - 1) / CB);
   const size_t lds = sizeof(float2) * (S + (size_t)CB * lp_row(S));

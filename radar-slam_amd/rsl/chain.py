@@ -103,6 +103,11 @@ class RadarChain:
 
     def run(self, cube, *, esprit: bool = True, velocity: bool = True):
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""
+        self.run_front(cube)
+        self.run_back(esprit=esprit, velocity=velocity)
+
+    def run_front(self, cube):
+        """Memory-bound half: RDS + detection, offsets, peak / cell compaction (current stream)."""
         ctx, cfg = self.ctx, self.cfg
         group = ctx.rds_detect(cube, self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds, work=self.work,
                                mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow,
@@ -110,6 +115,10 @@ class RadarChain:
         ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
         ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists,
                  peak_pow=self.peak_pow, peak_pow_group=group)
+
+    def run_back(self, *, esprit: bool = True, velocity: bool = True):
+        """Compute-bound half: DoA scan (+ ESPRIT, phase) and the velocity solve, on run_front's lists."""
+        ctx, cfg = self.ctx, self.cfg
         L = self.lists
         if self.fused_doa:
             ctx.doa_extras(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
