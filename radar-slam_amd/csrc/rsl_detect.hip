@@ -9,6 +9,8 @@
 // Per-antenna 64-bit ballots give one mask word per 64 Doppler cells; a per-frame scan then turns
 // row counts into entry offsets (antenna-major) and union-cell offsets (range-major), and the emit
 // kernel writes both lists in reference order without any sort.
+#include <cstdlib>
+
 #include "rsl_common.h"
 #include "rsl_internal.h"
 
@@ -395,6 +397,75 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   }
 }
 
+// Cell-list compaction (union masks, ~54 % dense at cfg2): 4 threads per mask word (16-bit slices), 64 words per
+// block, so every block's items (at most 4096) are expanded in one round and no thread walks more than 16 set bits
+// (k_emit_block's word-per-thread cells path walked ~35 bits per word, up to 5 rounds of 2048 per block).
+// Blocks are row- and frame-aligned ((S * W) % 64 == 0): one contiguous run of cells from cell_base[f] + row offset.
+constexpr int kCellWords = 64;
+constexpr int kCellCap = kCellWords * 64;
+
+template <int W, int MAXA>
+__global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __restrict__ mask,
+                                                    const unsigned long long* __restrict__ umask, long long F, int A,
+                                                    int S, int C, const int* __restrict__ cell_row_off,
+                                                    const long long* __restrict__ cell_base, long long cell_cap,
+                                                    int* __restrict__ c_frame, int* __restrict__ c_rc,
+                                                    unsigned* __restrict__ c_amask) {
+  __shared__ unsigned pk[kCellCap];   // item code: (thread << 4) | bit within the thread's 16-bit slice
+  __shared__ unsigned pam[kCellCap];  // antenna mask of the item's cell
+  __shared__ int wsum[4];
+  __shared__ long long s_first;
+  const int t = threadIdx.x;
+  const long long ncw = F * S * W;
+  const long long gw0 = (long long)blockIdx.x * kCellWords;
+  const int wl = t >> 2, sl = t & 3;
+  const bool valid = gw0 + wl < ncw;
+  const long long gw = valid ? gw0 + wl : gw0;
+  const long long row = gw / W;  // f * S + i
+  const int w = (int)(gw - row * W);
+  const long long f = row / S;
+  const int i = (int)(row - f * S);
+  unsigned long long m = valid ? umask[gw] : 0ull;
+  unsigned long long ma[MAXA];
+#pragma unroll
+  for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
+  if (t == 0) s_first = cell_base[f] + cell_row_off[row];
+  const unsigned sm16 = (unsigned)(m >> (16 * sl)) & 0xffffu;
+  int total;
+  const int loc = block_exclusive_scan(__popc(sm16), wsum, total);
+  {
+    unsigned mm = sm16;
+    int o = loc;
+    while (mm) {
+      const int b = __ffs(mm) - 1;
+      mm &= mm - 1;
+      const int bit = 16 * sl + b;
+      unsigned am = 0;
+#pragma unroll
+      for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> bit) & 1ull) << aa;
+      pk[o] = ((unsigned)t << 4) | (unsigned)b;
+      pam[o] = am;
+      ++o;
+    }
+  }
+  __syncthreads();
+  const long long first = s_first;
+  for (int k = t; k < total; k += 256) {
+    const long long e = first + k;
+    if (e < cell_cap) {
+      const unsigned code = pk[k];
+      const int tt = (int)(code >> 4);
+      const long long g2 = gw0 + (tt >> 2);
+      const long long rw = g2 / W;
+      const int ww = (int)(g2 - rw * W);
+      const long long ff = rw / S;
+      c_frame[e] = (int)ff;
+      c_rc[e] = (int)(rw - ff * S) * C + ww * 64 + 16 * (tt & 3) + (int)(code & 15);
+      c_amask[e] = pam[k];
+    }
+  }
+}
+
 hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
                         const float* pk_pow, int pk_group, int F, int A, int S, int C, const int* entry_row_off,
                         const int* cell_row_off, const long long* entry_base, const long long* cell_base,
@@ -403,8 +474,31 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   if (F <= 0) return hipSuccess;
   if (A > 32) return hipErrorInvalidValue;
   const int W = (C + 63) / 64;
-  const long long nbe = ((long long)F * A * S * W + 255) / 256, nbc = ((long long)F * S * W + 255) / 256;
+  const long long nbe = ((long long)F * A * S * W + 255) / 256;
+  // cells: k_emit_cells when its frame-aligned blocks tile the cell words (RSL_EMIT_CELLS=0: the word-per-thread path)
+  const char* ec = getenv("RSL_EMIT_CELLS");
+  const bool cells4 = ((long long)S * W) % kCellWords == 0 && !(ec && atoi(ec) == 0);
+  const long long nbc = cells4 ? 0 : ((long long)F * S * W + 255) / 256;
   const unsigned nb = (unsigned)(nbe + nbc);
+  if (cells4) {
+    const unsigned nbc4 = (unsigned)(((long long)F * S * W) / kCellWords);
+#define GOC(WW)                                                                                                  \
+  hipLaunchKernelGGL((A <= 8 ? k_emit_cells<WW, 8> : k_emit_cells<WW, 32>), dim3(nbc4), dim3(256), 0, st, mask,  \
+                     umask, (long long)F, A, S, C, cell_row_off, cell_base, cell_cap, c_frame, c_rc, c_amask);
+    switch (W) {
+      case 1: GOC(1) break;
+      case 2: GOC(2) break;
+      case 4: GOC(4) break;
+      case 8: GOC(8) break;
+      case 16: GOC(16) break;
+      case 32: GOC(32) break;
+      case 64: GOC(64) break;
+      default: return hipErrorInvalidValue;
+    }
+#undef GOC
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
 #define GO(WW)                                                                                                   \
   hipLaunchKernelGGL((A <= 8 ? k_emit_block<WW, 8> : k_emit_block<WW, 32>), dim3(nb), dim3(256), 0, st, mask,    \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
