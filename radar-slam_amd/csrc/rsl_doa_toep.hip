@@ -34,15 +34,15 @@ constexpr float kToepScale = 256.f;
 
 // The Toeplitz B column of one cell: e = [r0, Re r1, Im r1, ..., Re r_{M-1}, Im r_{M-1}, 0...] of the unit-norm
 // signature, scaled by 2^8 (exact), fp32.
-template <int MA, int KB>
-RSL_DEV void toep_entries(const float2 (&s)[MA], float (&e)[16 * KB]) {
+// Autocorrelation of the raw signature, r_k = sum_n s_{n+k} conj(s_n) (k = 0..MA-1; r_0 = |s|^2 real): shared by the
+// Toeplitz column, ESPRIT and (through s) the spatial phase.
+template <int MA>
+RSL_DEV void acf(const float2 (&s)[MA], float (&ar)[MA], float (&ai)[MA]) {
   float pw = 0.f;
 #pragma unroll
   for (int m = 0; m < MA; ++m) pw = fmaf(s[m].x, s[m].x, fmaf(s[m].y, s[m].y, pw));
-  // angle_estimation.py:86-88 (unit-norm s).  v_rcp_f32 (1 ulp): a common scale of all of a cell's grid values
-  // cannot move its argmax, and the MUSIC degeneracy test has a 1e-4 margin
-  const float inv = pw > 0.f ? kToepScale * __builtin_amdgcn_rcpf(pw) : 0.f;
-  e[0] = pw > 0.f ? kToepScale : 0.f;
+  ar[0] = pw;
+  ai[0] = 0.f;
 #pragma unroll
   for (int k = 1; k < MA; ++k) {
     float re = 0.f, im = 0.f;
@@ -51,11 +51,62 @@ RSL_DEV void toep_entries(const float2 (&s)[MA], float (&e)[16 * KB]) {
       re = fmaf(s[n + k].x, s[n].x, fmaf(s[n + k].y, s[n].y, re));
       im = fmaf(s[n + k].y, s[n].x, fmaf(-s[n + k].x, s[n].y, im));
     }
-    e[2 * k - 1] = re * inv;
-    e[2 * k] = im * inv;
+    ar[k] = re;
+    ai[k] = im;
+  }
+}
+
+// The Toeplitz B column of one cell: e = [r0, Re r1, Im r1, ..., Re r_{M-1}, Im r_{M-1}, 0...] of the unit-norm
+// signature, scaled by 2^8 (exact), fp32.  inv = 2^8 / |s|^2 (0 for a zero signature).
+template <int MA, int KB>
+RSL_DEV void toep_entries(const float (&ar)[MA], const float (&ai)[MA], float inv, float (&e)[16 * KB]) {
+  // angle_estimation.py:86-88 (unit-norm s).  v_rcp_f32 (1 ulp): a common scale of all of a cell's grid values
+  // cannot move its argmax, and the MUSIC degeneracy test has a 1e-4 margin
+  e[0] = ar[0] > 0.f ? kToepScale : 0.f;
+#pragma unroll
+  for (int k = 1; k < MA; ++k) {
+    e[2 * k - 1] = ar[k] * inv;
+    e[2 * k] = ai[k] * inv;
   }
 #pragma unroll
   for (int x = 2 * MA - 1; x < 16 * KB; ++x) e[x] = 0.f;
+}
+
+// ESPRIT (angle_estimation.py:178-225) for a full array (A = M) from the autocorrelation: the 2x2 Gram matrix of
+// X = [s[:-1], s[1:]] is [[r0 - |s_{M-1}|^2, r1], [conj r1, r0 - |s_0|^2]], and with u_m = v0 s_m + v1 s_{m+1} the
+// sums phi = sum_{m<M-2} conj(u_m) u_{m+1} and d = sum_{m<M-2} |u_m|^2 expand into r0, r1, r2 and edge products:
+//   phi = |v0|^2 (r1 - conj(s_{M-2}) s_{M-1}) + conj(v0) v1 r2 + conj(v1) v0 (r0 - |s_0|^2 - |s_{M-1}|^2)
+//         + |v1|^2 (r1 - conj(s_0) s_1)
+//   d   = |v0|^2 (r0 - |s_{M-2}|^2 - |s_{M-1}|^2) + |v1|^2 (r0 - |s_0|^2 - |s_{M-1}|^2)
+//         + 2 Re(conj(v0) v1 (r1 - conj(s_{M-2}) s_{M-1}))
+// (O(1) work instead of esprit_phi's O(M) passes; all terms share the scale sc, which cancels in angle(phi)).
+template <int MA>
+RSL_DEV void esprit_acf(const float2 (&s)[MA], const float (&ar)[MA], const float (&ai)[MA], float sc, float& nr,
+                        float& ni, float& dd) {
+  static_assert(MA >= 3, "ESPRIT from the autocorrelation needs M >= 3");
+  const float2 s0 = s[0], s1 = s[1], sl = s[MA - 1], sl2 = s[MA - 2];
+  const float r0 = ar[0] * sc, r1r = ar[1] * sc, r1i = ai[1] * sc, r2r = ar[2] * sc, r2i = ai[2] * sc;
+  const float e0 = cabs2(s0) * sc, el = cabs2(sl) * sc, el2 = cabs2(sl2) * sc;
+  // conj(s_{M-2}) s_{M-1}, conj(s_0) s_1
+  const float tr = (sl2.x * sl.x + sl2.y * sl.y) * sc, ti = (sl2.x * sl.y - sl2.y * sl.x) * sc;
+  const float hr = (s0.x * s1.x + s0.y * s1.y) * sc, hi = (s0.x * s1.y - s0.y * s1.x) * sc;
+  const float a = r0 - el, cc = r0 - e0, br = r1r, bi = r1i;
+  const float hd = 0.5f * (a - cc);
+  const float l1 = 0.5f * (a + cc) + sqrtf(hd * hd + br * br + bi * bi);
+  float v0r, v0i, v1r, v1i;
+  if (a >= cc) {  // v = [l1 - c, conj(b)]
+    v0r = l1 - cc; v0i = 0.f; v1r = br; v1i = -bi;
+  } else {        // v = [b, l1 - a]
+    v0r = br; v0i = bi; v1r = l1 - a; v1i = 0.f;
+  }
+  const float n0 = v0r * v0r + v0i * v0i, n1 = v1r * v1r + v1i * v1i;
+  const float cr = v0r * v1r + v0i * v1i, ci = v0r * v1i - v0i * v1r;  // conj(v0) v1
+  const float sar = r1r - tr, sai = r1i - ti;                          // r1 - conj(s_{M-2}) s_{M-1}
+  const float scc = r0 - e0 - el;
+  const float sdr = r1r - hr, sdi = r1i - hi;                          // r1 - conj(s_0) s_1
+  nr = n0 * sar + (cr * r2r - ci * r2i) + cr * scc + n1 * sdr;         // conj(v1) v0 = conj(conj(v0) v1)
+  ni = n0 * sai + (cr * r2i + ci * r2r) - ci * scc + n1 * sdi;
+  dd = n0 * (r0 - el2 - el) + n1 * scc + 2.f * (cr * sar - ci * sai);
 }
 
 // fp16 hi/lo split of 8 consecutive entries, packed two halves per dword (4 + 4 dwords).
@@ -210,29 +261,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
       const long long c2 = nx * 64 + lane;
       load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns);
     }
+    float ar[MA], ai[MA];
+    acf<MA>(s, ar, ai);
+    const float inv = ar[0] > 0.f ? kToepScale * __builtin_amdgcn_rcpf(ar[0]) : 0.f;
     if constexpr (EXTRAS) {
       // fused K6 (k_cell_extras) for the own cell, before the scan so its registers are dead during the MFMA
       // loop: ESPRIT (angle_estimation.py:178-225) and the spatial phase angle(s1 conj(s0)) (velocity_solver.py
-      // :136); fp32 closed form from the fp32 signature.
-      float sr[MA], si[MA], pw = 0.f;
-#pragma unroll
-      for (int m = 0; m < MA; ++m) {
-        sr[m] = s[m].x;
-        si[m] = s[m].y;
-        pw = fmaf(sr[m], sr[m], fmaf(si[m], si[m], pw));
-      }
-      if (pw > 0.f) {
-        const float sc = __builtin_amdgcn_rsqf(pw);  // ESPRIT and the phase are invariant to the scale
-#pragma unroll
-        for (int m = 0; m < MA; ++m) {
-          sr[m] *= sc;
-          si[m] *= sc;
-        }
-      }
+      // :136); fp32 closed forms from the fp32 signature (both invariant to its scale).
       if (c < ncell) {
         if (out_esprit) {
           float nr, ni, dd;
-          esprit_phi<MA>(sr, si, A, nr, ni, dd);
+          if (A == MA) {
+            esprit_acf<MA>(s, ar, ai, inv * (1.f / kToepScale), nr, ni, dd);
+          } else {  // fewer antennas than the template width: the general per-element form
+            float sr[MA], si[MA];
+            const float sc = ar[0] > 0.f ? __builtin_amdgcn_rsqf(ar[0]) : 1.f;
+#pragma unroll
+            for (int m = 0; m < MA; ++m) {
+              sr[m] = s[m].x * sc;
+              si[m] = s[m].y * sc;
+            }
+            esprit_phi<MA>(sr, si, A, nr, ni, dd);
+          }
           const float ang = dd > 0.f ? atan2f(ni, nr) : 0.f;
           // fp32 asin (the input angle is fp32 already; tolerance 1e-3 rad).  For d >= lambda/2 the reference's
           // argument never exceeds 1 (|angle| <= pi): clamp the fp32 rounding of pi * scale there; for d < lambda/2
@@ -241,7 +291,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
           if (esprit_scale * 3.14159265358979323846 <= 1.0 + 1e-9) x = fminf(fmaxf(x, -1.f), 1.f);
           out_esprit[c] = (double)(asinf(x) * 57.2957795130823208768f);
         }
-        if (out_phase) out_phase[c] = (double)atan2f(si[1] * sr[0] - sr[1] * si[0], sr[1] * sr[0] + si[1] * si[0]);
+        if (out_phase)
+          out_phase[c] = (double)atan2f(s[1].y * s[0].x - s[1].x * s[0].y, s[1].x * s[0].x + s[1].y * s[0].y);
       }
     }
     // B operands of the two column tiles: own K half from the own cell, the other half from lane ^ 32
@@ -252,7 +303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
 #pragma unroll
         for (int x = 0; x < 16 * KB; ++x) e[x] = s[x % MA].x;
       } else {
-        toep_entries<MA, KB>(s, e);
+        toep_entries<MA, KB>(ar, ai, inv, e);
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
