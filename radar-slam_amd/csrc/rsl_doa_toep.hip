@@ -359,6 +359,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     // a v_cndmask per value
     auto record = [&](int t, const floatx16& acc0, const floatx16& acc1) {
       const float m0 = tile_max(acc0), m1 = tile_max(acc1);
+      if (NTC > 0 && t == 0) {  // unrolled: the first tile is always the record (no branch, no initial copies)
+        typedef double doublex8 __attribute__((ext_vector_type(8)));
+        const doublex8 d0 = __builtin_bit_cast(doublex8, acc0), d1 = __builtin_bit_cast(doublex8, acc1);
+        best0 = m0;
+        best1 = m1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sv0[k] = d0[k];
+          sv1[k] = d1[k];
+        }
+        return;
+      }
       if (m0 > best0) {
         best0 = m0;
         bt0 = t;
