@@ -230,6 +230,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
                                                   float* __restrict__ out_gmax, double esprit_scale,
                                                   double* __restrict__ out_esprit, double* __restrict__ out_phase) {
   extern __shared__ uint4 tt[];  // the whole Toeplitz operand table (<= 64 KiB)
+  {
+    const long long nc = ncell_dev ? *ncell_dev : ncell_host;
+    if ((long long)blockIdx.x * 256 >= nc) return;  // a block past the cells (capacity-sized grids): no table load
+  }
   const int nvec = ntiles * KB * 2 * 64;
   for (int x = threadIdx.x; x < nvec; x += 256) tt[x] = ttab[x];
   __syncthreads();
@@ -461,6 +465,12 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   long long blocks = (long long)nb * ncu;
   if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+  // Grid sized from the cell count (the capacity when the count is on the device; blocks past the cells exit before
+  // loading the table) with ~8 passes per wave, instead of a persistent grid of resident blocks: measured 1.52-1.56
+  // vs 1.71-1.79 ms per 1000 cfg2 frames.  RSL_DOA_PPW=0 restores the persistent grid.
+  const char* eppw = getenv("RSL_DOA_PPW");
+  const int ppw = eppw ? atoi(eppw) : 8;
+  if (ppw > 0) blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
                      ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase);
