@@ -257,17 +257,38 @@ def main():
         per = lambda name: kt[name][0] / max(kt[name][1], 1)  # ms per launch
         Fl = F // NS
         ncl = nc / NS                                          # unique cells per launch
-        # Dominant kernel: the fused DoA scan (k_doa_toep).  Algorithmic work of its formulation: one real dot
-        # product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2), evaluated as three f16
-        # MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops; bound: dense f16 MFMA peak.
-        t_doa = per('doa_scan') * 1e-3
+        # Roofline entries of the three big kernels.  Algorithmic work per launch (per kernel):
+        #  K1 k_range_fft_p: read the c64 cube + write the c64 range spectra  = 2 A C S 8 bytes per frame
+        #  K2 k_doppler_detect: read the range spectra + write the c64 RDS    = 2 A C S 8 bytes per frame
+        #     (masks / peak powers, ~1 %, not counted)
+        #  K5 k_doa_toep: one real dot product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2),
+        #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
+        src_std = ks if ks else kt
+        per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
         flops = 3 * 2 * (2 * A - 1) * ncl * G
-        ach = flops / t_doa / 1e12
-        line["roofline"] = {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                            "traffic": pmc_traffic('k_doa_toep', Fl), "avg_launch_ms": per('doa_scan'),
-                            "algorithmic_flops_per_launch": flops,
-                            "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
+        kbytes = 2 * A * C * S * 8 * Fl
+
+        def entry(name, ms):
+            if name == 'doa_scan':
+                ach = flops / (ms * 1e-3) / 1e12
+                return {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                        "traffic": pmc_traffic('k_doa_toep', Fl), "avg_launch_ms": ms,
+                        "algorithmic_flops_per_launch": flops,
+                        "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
+            kern = {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'}[name]
+            ach = kbytes / (ms * 1e-3) / 1e9
+            return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl), "avg_launch_ms": ms,
+                    "algorithmic_bytes_per_launch": kbytes}
+
+        # dominant kernel = the longest standalone launch (the pipelined timed region overlaps K1 of one batch with
+        # the DoA scan of the previous one, which stretches K1's live duration); its figures use the live average
+        # launch duration over the timed region, as measured by hipEvents on its stream
+        big = ('range_fft', 'doppler_fft', 'doa_scan')
+        dom = max(big, key=per_std)
+        line["roofline"] = entry(dom, per(dom))
+        line["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big}
         # FFT stage (K1 + K2/K3): HBM-bound; algorithmic bytes = read the c64 cube + write the c64 RDS.  Timed on
         # standalone launches when the timed region is pipelined (there K1 shares the GPU with the DoA scan)
         src = ks if ks else kt
