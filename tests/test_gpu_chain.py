@@ -21,6 +21,7 @@ CFGS = {  # name: (A, C, T_c)
     'cfg5a16': (16, 32, 12.8e-6),
     'cfg5': (16, 256, 102.4e-6),  # configs[4] frame shape (A16 C256 S1024), one frame
     'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
+    'a4': (4, 64, 25.6e-6),  # fewer antennas than the DoA kernel's width (zero-padded signature, per-element ESPRIT)
 }
 FRAMES = {'cfg5': 1}
 DOA_SAMPLE = 30000  # cells checked per frame against the oracle scan (random subset above this; cfg5 has ~207 K)
