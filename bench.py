@@ -32,9 +32,15 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:
 PROFILE = os.path.join(ROOT, 'profiles', 'r1g_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
-def pmc_traffic(kernel_prefix, frames_per_launch):
+PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
+
+
+def pmc_traffic(kernel_prefix, frames_per_launch, config='cfg2'):
     """HBM bytes per launch of a kernel from the committed PMC profile (FETCH_SIZE x 2 + WRITE_SIZE, per
-    MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present."""
+    MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present or the profile was
+    collected on another workload."""
+    if config != PROFILE_CONFIG:
+        return None
     try:
         prof = json.load(open(PROFILE))
     except (OSError, ValueError):
@@ -110,7 +116,11 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--frames-per-step', type=int, default=1000)
+    ap.add_argument('--frames-per-step', type=int, default=None,
+                    help='frames per GPU per step (default 1000 for cfg2, 100 for cfg5)')
+    ap.add_argument('--config', choices=('cfg2', 'cfg5'), default='cfg2',
+                    help='cfg2 = configs[2] (A8 C128 S512, the metric\'s workload); cfg5 = the configs[4] frame shape '
+                         '(A16 C256 S1024), a second measurement, not the metric line')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--no-timing', action='store_true', help='disable per-kernel hipEvent timing')
@@ -140,8 +150,11 @@ def main():
     torch.cuda.set_device(dev)
 
     import rsl
-    A, C, S, F = 8, 128, 512, args.frames_per_step
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=51.2e-6)
+    if args.config == 'cfg5':
+        A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 100
+    else:
+        A, C, S, Tc, F = 8, 128, 512, 51.2e-6, args.frames_per_step or 1000
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
     ctx = rsl.get_context(local)
     NS = max(1, args.streams)
     if F % NS:
@@ -245,7 +258,8 @@ def main():
         "metric": METRIC, "value": fps, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "configs[2]: 8ch x 128chirp x 512 synthetic cube, full chain "
+        "config": {"workload": ("configs[2]: 8ch x 128chirp x 512" if args.config == 'cfg2' else
+                                "configs[4] frame shape: 16ch x 256chirp x 1024") + " synthetic cube, full chain "
                                "(RDS + peaks + MUSIC argmax + ESPRIT + LS velocity + trajectory)",
                    "frames_per_step": F, "frames_per_gpu_per_step": F, "antennas": A, "chirps": C, "samples": S,
                    "doa_grid": G, "streams_per_gpu": 2 if args.pipeline else NS,
@@ -273,13 +287,13 @@ def main():
                 ach = flops / (ms * 1e-3) / 1e12
                 return {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                        "traffic": pmc_traffic('k_doa_toep', Fl), "avg_launch_ms": ms,
+                        "traffic": pmc_traffic('k_doa_toep', Fl, args.config), "avg_launch_ms": ms,
                         "algorithmic_flops_per_launch": flops,
                         "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
             kern = {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'}[name]
             ach = kbytes / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl), "avg_launch_ms": ms,
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, args.config), "avg_launch_ms": ms,
                     "algorithmic_bytes_per_launch": kbytes}
 
         # dominant kernel = the longest standalone launch (the pipelined timed region overlaps K1 of one batch with
