@@ -368,8 +368,6 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) {
-    const int i = i0 + rb + rr;
-    const size_t row = (size_t)fa * S + i;
     int off = pre, cnt = 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -379,11 +377,19 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
     }
     pre += cnt;
     const unsigned long long b = wb[(rb + rr) * NCH + ch];
-    if (DBG != 5 && lane == 0) {  // DBG 5: no mask / count stores (ablation)
-      mask[row * NCH + ch] = b;
-      if (ch == 0) row_count[row] = cnt;
-    }
     if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(b & ((1ull << lane) - 1ull))] = p[rr + 1];
+  }
+  // the tile's mask words and row counts from the ballots in LDS, one coalesced store each (the tile's shifted rows
+  // i0 .. i0 + KB - 1 are contiguous), instead of single-lane stores per row and wave
+  if (DBG != 5) {  // DBG 5: no mask / count stores (ablation)
+    const size_t row0 = (size_t)fa * S + i0;
+    if (tid < KB * NCH) mask[row0 * NCH + tid] = wb[tid];
+    if (tid < KB) {
+      int cnt = 0;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) cnt += __popcll(wb[tid * NCH + c]);
+      row_count[row0 + tid] = cnt;
+    }
   }
 }
 
