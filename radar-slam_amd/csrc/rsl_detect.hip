@@ -266,7 +266,8 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   __shared__ unsigned pk[kEmitCap];   // item code: (word << 6) | bit
   __shared__ unsigned pam[kEmitCap];  // cells: antenna mask of the item
   __shared__ int wsum[4];
-  __shared__ int s_loc[256], s_cw[256], s_r0[256], s_fi[256];
+  __shared__ int s_cw[256], s_fi[256];
+  __shared__ long long s_pkb[256];  // entries: peak_pow index of the word's item 0 minus its block rank
   __shared__ unsigned long long s_u[256];
   __shared__ long long s_first;
   const int t = threadIdx.x, lane = t & 63;
@@ -313,11 +314,12 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
   // entries: peaks of the earlier words of this row (the row's words are lanes lane-w .. lane of this wave)
   const int r0 = loc - __shfl(loc, lane - w);
   if (t == 0) s_first = fst;
-  s_loc[t] = loc;
-  s_r0[t] = r0 + gof;
   s_cw[t] = (int)(cwb + cwo);
   s_u[t] = u;
   s_fi[t] = entries ? ((a << 16) | i) : (int)f;
+  // the row's group starts at row - i % pk_group; item k of the block reads peak_pow[s_pkb + base + k] (divisions once
+  // per word instead of 64-bit divisions per item)
+  if (entries) s_pkb[t] = (row - i % pk_group) * (long long)C + (r0 + gof) - loc;
   // rounds of kEmitCap items (one round unless the block is dense, e.g. the cell union at high peak density)
   for (int base = 0; base < total; base += kEmitCap) {
     // phase 1: packed (word, bit) codes (+ the cell's antenna mask) of this round's items, in LDS
@@ -352,11 +354,7 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
           const int k = k0 + 256 * uu;
           pw[uu] = 0.f;
           if (k < nk && e_pdb) {
-            const unsigned code = pk[k];
-            const int tt = (int)(code >> 6);
-            const long long rw = (gw0 + tt) / W;  // row (f A + a) S + i; its group's first row holds slot 0
-            const long long rg = rw - (rw % S) % pk_group;
-            pw[uu] = pk_pow[(size_t)rg * C + s_r0[tt] + (base + k - s_loc[tt])];
+            pw[uu] = pk_pow[s_pkb[pk[k] >> 6] + base + k];
           }
         }
 #pragma unroll
