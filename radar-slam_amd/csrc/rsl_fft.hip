@@ -678,6 +678,9 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       return hipGetLastError();
     };
     if constexpr (S == 512) {  // RSL_RF_CB: chirp rows per tile (4 / 8 / 16) for tuning
+      // 16 rows (78 KiB LDS, 16 float4 in flight per thread) is faster alone (1.53 vs 1.63 ms per 1000 cfg2 frames,
+      // tools/rf_ab.py) but leaves no LDS for the previous batch's DoA blocks in the pipelined chain (153 k vs
+      // 171 k frames/s), so 8 rows stay the default
       const char* e = getenv("RSL_RF_CB");
       const int v = e ? atoi(e) : CB;
       if (v == 4) return go(std::integral_constant<int, 4>{});
