@@ -301,7 +301,7 @@ RSL_DEV void dd_tile_compute(float2* buf, const float2* tws, int S, int k0, unsi
 // column-wise 3-max over j-1, j, j+1; 'reflect' edges repeat the in-window cell).
 template <int C, int KB, int NT>
 constexpr bool dd_reg_ok() {
-  return C % 64 == 0 && KB % 8 == 0 && (C / 64) * (KB / 8) * 64 == NT;
+  return C % 64 == 0 && KB % 8 == 0 && (C / 64) * (KB / 8) * 64 == NT && KB * (C / 64) <= 64;
 }
 
 template <int C, int KB, int NT, int DBG = 0>
@@ -363,8 +363,10 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   __syncthreads();
   // peak powers compact over the tile's KB rows (one contiguous run from the tile's first row slot): the peaks
   // of the rows before this wave's first row, then row by row
-  int pre = 0;
-  for (int x = 0; x < rb * NCH; ++x) pre += __popcll(wb[x]);
+  // (the tile's KB * NCH <= 64 ballot words: one per lane, summed across the wave instead of a serial LDS loop)
+  int pre = lane < rb * NCH ? __popcll(wb[lane]) : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) pre += __shfl_xor(pre, off);
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) {
