@@ -136,13 +136,16 @@ RSL_DEV void swap32_u4(uint4& a, uint4& b) {
   b = make_uint4(bv[0], bv[1], bv[2], bv[3]);
 }
 
-template <int MA>
-RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
-                        long long c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
-  // loads from always-valid addresses (cell 0 past the end: its results are never stored); antennas past A
-  // (A < MA, wave-uniform) are clamped to A-1 and zeroed
+// The cell's (frame, range * C + doppler) pair; past the end: cell 0 (its results are never stored).
+RSL_DEV int2 load_cell(const int* __restrict__ cfr, const int* __restrict__ crc, long long c, bool ok) {
   const long long cc = ok ? c : 0;
-  const float2* base = rds + (size_t)cfr[cc] * fstride + crc[cc];
+  return make_int2(cfr[cc], crc[cc]);
+}
+
+// Signature of a cell from its (frame, rc) pair; antennas past A (A < MA, wave-uniform) are clamped to A-1 and zeroed.
+template <int MA>
+RSL_DEV void load_sig_at(const float2* __restrict__ rds, int2 fr, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
+  const float2* base = rds + (size_t)fr.x * fstride + fr.y;
   if (A >= MA) {
 #pragma unroll
     for (int m = 0; m < MA; ++m) s[m] = base[(size_t)m * plane];
@@ -153,6 +156,12 @@ RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ 
       s[m] = m < A ? z : make_float2(0.f, 0.f);
     }
   }
+}
+
+template <int MA>
+RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
+                        long long c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
+  load_sig_at<MA>(rds, load_cell(cfr, crc, c, ok), A, plane, fstride, s);
 }
 
 // Max of one 32x32 tile's 16 values held by this lane, as signed-integer max3 on the float bits (v_max3_i32):
@@ -245,7 +254,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
   const long long stride = (long long)gridDim.x * 4;
   long long ch = (long long)blockIdx.x * 4 + wave;
   const float mthr = ((float)A - 1e-4f) * kToepScale;
+  // Two-level prefetch: the signature of the next pass is loaded during this pass from cell indices that were loaded
+  // one pass earlier (index loads followed at once by the dependent signature loads stalled every pass for a full
+  // memory round trip).
   float2 ns[MA];
+  int2 nidx = make_int2(0, 0);
   if (ch < nch) {
     const long long c = ch * 64 + lane;
     if constexpr (DBG == 3) {
@@ -253,6 +266,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
       for (int m = 0; m < MA; ++m) ns[m] = make_float2(0.1f * (lane + m), 0.2f * m - lane * 0.01f);
     } else {
       load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
+      const long long c2 = (ch + stride) * 64 + lane;
+      if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
     }
   }
   for (; ch < nch; ch += stride) {
@@ -261,9 +276,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     for (int m = 0; m < MA; ++m) s[m] = ns[m];
     const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
-    if (nx < nch && DBG != 3) {  // prefetch the next pass's signatures while this pass's scan runs
-      const long long c2 = nx * 64 + lane;
-      load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns);
+    if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
+      load_sig_at<MA>(rds, nidx, A, plane, fstride, ns);
+      const long long c3 = (nx + stride) * 64 + lane;
+      if (nx + stride < nch) nidx = load_cell(cfr, crc, c3, c3 < ncell);
     }
     float ar[MA], ai[MA];
     acf<MA>(s, ar, ai);
@@ -448,10 +464,12 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   if constexpr (MUSIC && !GMAX && !EXTRAS && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing studies only)
     if (const char* e = getenv("RSL_DOA_DBG")) {
       const int v = atoi(e);
-      if (v == 1) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 1>;
-      if (v == 2) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 2>;
-      if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3>;
-      if (v == 4) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 4>;
+      if (ntiles == 12) {  // the unrolled form the bench runs
+        if (v == 1) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 1, 12>;
+        if (v == 2) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 2, 12>;
+        if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3, 12>;
+        if (v == 4) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 4, 12>;
+      }
     }
   }
   const size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);

@@ -5,11 +5,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, 'radar-slam_amd'), ROOT]
 import torch, rsl
 from bench import make_cubes
-F = int(os.environ.get('F', '200'))
+F = int(os.environ.get('F', '1000'))
 ctx = rsl.get_context(0)
 cfg = rsl.ChainConfig(num_antennas=8, num_chirps=128, chirp_duration=51.2e-6)
 ch = rsl.RadarChain(cfg, F, ctx)
-cube = make_cubes(torch, torch.device('cuda', 0), 1, F, 8, 128, 512, 5)[0]
+cube = make_cubes(ctx, 1, F, 8, 128, 51.2e-6, 0)[0]
 ch.run(cube)
 torch.cuda.synchronize()
 L = ch.lists
