@@ -11,7 +11,11 @@
  *     complex values are interleaved float32 (c64) unless the name says c128 / f64;
  *   - all launches are asynchronous on the handle's stream (rsl_set_stream); rsl_sync waits;
  *   - return 0 (RSL_OK) or an RSL_ERR_* code; rsl_last_error(h) describes the last failure;
- *   - one handle per (device, stream); handles share no mutable state.
+ *   - one handle per (device, stream); handles share no mutable state;
+ *   - F = 0 (an empty batch) is valid: nothing is launched (rsl_peak_offsets zeroes the two bases), and
+ *     buffers sized by F may be null;
+ *   - capacity-sized lists (entries, cells) never overflow in memory: items past the capacity are dropped,
+ *     the bases keep the true counts, and the list consumers stop at the capacity.
  */
 #ifndef RSL_H
 #define RSL_H
@@ -121,7 +125,8 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
 
 /* a11-a16  extract_spatial_signature + music_spectrum / estimate_angle_music / estimate_angle_beamforming
  *     (angle_estimation.py:67-176, 227-251; robust_angle_estimation.py:236-245).
- *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = *ncell_dev if non-null else ncell.
+ *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = min(*ncell_dev, ncell) if ncell_dev is non-null
+ *     (ncell = the lists' capacity: an overflowed list is processed up to its capacity), else ncell.
  *     steer_tab = device copy of the rsl_steer_table_build output; steer_c128 = device fp64 [G][M][2]
  *     steering matrix (needed by MUSIC with RSL_DOA_TOEPLITZ for its exact fp64 near-degenerate re-scan).
  *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; ignored when out_spec is requested).
@@ -156,12 +161,13 @@ int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const voi
 /* a25-a29  VelocitySolver.two_step_optimization / solve_velocity (velocity_solver.py:65-355): exact
  *     box-constrained LS for (v_x, v_y) per segment (segments = frames).  az f64 [N] radians, or (when gidx
  *     i32 [N] is non-null) az = az_table[gidx] with az_table f64 [G], G <= 2048; y f64 [N]
- *     observed phase, amask u32 [N] (nullable; multiplicity = popcount), seg i64 [F+1],
+ *     observed phase, amask u32 [N] (nullable; multiplicity = popcount), seg i64 [F+1] (device; bounds
+ *     clamped to n = N, the arrays' length: a capacity-sized list that overflowed ends at its capacity),
  *     k = 4 pi dt / lambda, ridge >= 0, bounds4 (host) = {vx_lo, vx_hi, vy_lo, vy_hi};
  *     out f64 [F, 8] = {vx, vy, cost, rmse, max_residual, n, det, 0}; resid/pred f64 [N] nullable. */
 int rsl_velocity(rsl_handle h, const void* az, const void* gidx, const void* az_table, int G, const void* y,
-                 const void* amask, const void* seg, int F, double k, double ridge, const double* bounds4, void* out,
-                 void* resid, void* pred);
+                 const void* amask, const void* seg, long long n, int F, double k, double ridge, const double* bounds4,
+                 void* out, void* resid, void* pred);
 
 /* a3-a6  SignalPreprocessor.dechirp_signal / apply_window / remove_dc / process_chirp (dechirp.py:85-166):
  *     out[r, s] = in[r, s] * table[s], then (dc != 0) minus the row's complex mean.  in/out c64 [rows, S]. */

@@ -180,11 +180,11 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || S <= 0 || C <= 0 || chirp0 < 0 || chirp0 + C > C_total)
     return fail(h, RSL_ERR_INVALID, "rsl_rds: bad shape");
+  if (F == 0) return RSL_OK;  // empty batch: the (zero-size) buffers may be null
   if (!cube || !table || !work || !rds) return fail(h, RSL_ERR_INVALID, "rsl_rds: null pointer");
   if (!rsl_fft_supported(S) || !rsl_fft_supported(C))
     return fail(h, RSL_ERR_UNSUPPORTED, "rsl_rds: FFT size not supported (S=" + std::to_string(S) +
                                             ", C=" + std::to_string(C) + ")");
-  if (F == 0) return RSL_OK;
   hipSetDevice(h->device);
   float2* tS = twiddles(h, S);
   float2* tC = twiddles(h, C);
@@ -209,15 +209,16 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
                    void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group) {
   if (!h) return RSL_ERR_INVALID;
   if (peak_pow_group) *peak_pow_group = 1;
+  if (F < 0 || A <= 0 || S <= 0 || C <= 0 || chirp0 < 0 || chirp0 + C > C_total)
+    return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: bad shape");
+  if (F == 0) return RSL_OK;  // empty batch: the (zero-size) buffers may be null
   if (!mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: null pointer");
-  if (!rsl::doppler_detect_supported(C, S) || A <= 0 || F < 0) {  // unfused: a7 then a8
+  if (!rsl::doppler_detect_supported(C, S)) {  // unfused: a7 then a8
     if (int r = rsl_rds(h, cube, F, A, C_total, chirp0, C, S, table, dc_removal, work, rds)) return r;
     return rsl_detect(h, rds, F, A, S, C, thr_power, i_lo, i_hi, mask, row_count, db_map, peak_pow);
   }
-  if (chirp0 < 0 || chirp0 + C > C_total) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: bad shape");
   if (!cube || !table || !work || !rds) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect: null pointer");
   if (!rsl_fft_supported(S)) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_rds_detect: FFT size not supported");
-  if (F == 0) return RSL_OK;
   hipSetDevice(h->device);
   float2* tS = twiddles(h, S);
   float2* tC = twiddles(h, C);
@@ -260,6 +261,7 @@ int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double
                void* mask, void* row_count, void* db_map, void* peak_pow) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_detect: bad shape");
+  if (F == 0) return RSL_OK;
   if (!rds || !mask || !row_count) return fail(h, RSL_ERR_INVALID, "rsl_detect: null pointer");
   if ((size_t)(18 * (size_t)C * 4) > 64 * 1024) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_detect: C too large");
   Scope sc(h, RSL_K_DETECT);
@@ -274,7 +276,8 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
                      void* frame_counts, void* union_mask) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || S <= 0 || C <= 0 || A > 32) return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: bad shape");
-  if (!mask || !row_count || !entry_row_off || !cell_row_off || !scratch || !entry_base || !cell_base || !frame_counts)
+  if (!entry_base || !cell_base) return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: null pointer");
+  if (F > 0 && (!mask || !row_count || !entry_row_off || !cell_row_off || !scratch || !frame_counts))
     return fail(h, RSL_ERR_INVALID, "rsl_peak_offsets: null pointer");
   if (F == 0) {
     hipSetDevice(h->device);
@@ -298,6 +301,7 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* u
                   void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
   if (!h) return RSL_ERR_INVALID;
   if (F < 0 || A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: bad shape");
+  if (F == 0) return RSL_OK;
   if (!mask || !entry_row_off || !cell_row_off || !entry_base || !cell_base)
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null pointer");
   if ((entry_cap > 0 && (!e_ant || !e_rbin || !e_dbin || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
@@ -468,18 +472,19 @@ int rsl_confidence(rsl_handle h, const void* rds, int A, int S, int C, const voi
 }
 
 int rsl_velocity(rsl_handle h, const void* az, const void* gidx, const void* az_table, int G, const void* y,
-                 const void* amask, const void* seg, int F, double k, double ridge, const double* bounds4, void* out,
-                 void* resid, void* pred) {
+                 const void* amask, const void* seg, long long n, int F, double k, double ridge, const double* bounds4,
+                 void* out, void* resid, void* pred) {
   if (!h) return RSL_ERR_INVALID;
-  if (F < 0 || (!az && !gidx) || !y || !seg || !bounds4 || !out)
-    return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
+  if (F < 0 || n < 0) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
+  if (F == 0) return RSL_OK;
+  if ((!az && !gidx) || !y || !seg || !bounds4 || !out) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad argument");
   if (gidx && (!az_table || G <= 0 || G > 2048)) return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad grid table");
   if (!(bounds4[0] <= bounds4[1]) || !(bounds4[2] <= bounds4[3]) || ridge < 0)
     return fail(h, RSL_ERR_INVALID, "rsl_velocity: bad bounds/ridge");
   Scope sc(h, RSL_K_VELOCITY);
   return hip_check(h,
                    rsl::launch_velocity(h->stream, (const double*)az, (const int*)gidx, (const double*)az_table, G,
-                                        (const double*)y, (const unsigned*)amask, (const long long*)seg, F, k, ridge,
+                                        (const double*)y, (const unsigned*)amask, (const long long*)seg, n, F, k, ridge,
                                         bounds4, (double*)out, (double*)resid, (double*)pred),
                    "velocity");
 }

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
     __syncthreads();
     st = sst;
   }
-  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, jj = lane & 15;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void k_doa_argmax(const float2* __restrict__ r
     __syncthreads();
     st = sst;
   }
-  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, jj = lane & 15;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void k_cell_extras(const float2* __restrict__ 
                                                      double* __restrict__ az_out) {
   constexpr int MA = NA > 0 ? NA : kMaxA;
   const int A = NA > 0 ? NA : A_rt;
-  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const long long ncell = list_count(ncell_dev, ncell_host);
   const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
   if (c >= ncell) return;
   const size_t plane = (size_t)S * C;

@@ -240,13 +240,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
                                                   double* __restrict__ out_esprit, double* __restrict__ out_phase) {
   extern __shared__ uint4 tt[];  // the whole Toeplitz operand table (<= 64 KiB)
   {
-    const long long nc = ncell_dev ? *ncell_dev : ncell_host;
+    const long long nc = list_count(ncell_dev, ncell_host);
     if ((long long)blockIdx.x * 256 >= nc) return;  // a block past the cells (capacity-sized grids): no table load
   }
   const int nvec = ntiles * KB * 2 * 64;
   for (int x = threadIdx.x; x < nvec; x += 256) tt[x] = ttab[x];
   __syncthreads();
-  const long long ncell = ncell_dev ? *ncell_dev : ncell_host;
+  const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;

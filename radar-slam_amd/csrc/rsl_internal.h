@@ -5,6 +5,14 @@
 
 namespace rsl {
 
+// Cell count of a capacity-sized list: the device count (written by the emit stage) clamped to the list capacity,
+// so an overflowing batch reads and writes only the slots that exist (the host sees the overflow in the count).
+__device__ __forceinline__ long long list_count(const long long* dev, long long cap) {
+  if (!dev) return cap;
+  const long long n = *dev;
+  return n < cap ? n : cap;
+}
+
 // K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
 // cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
@@ -74,7 +82,8 @@ hipError_t launch_confidence(hipStream_t st, const float2* rds, int A, int S, in
                              const double* steer_phase, double* conf_out);
 // K8: batched bounded / ridge least squares velocity solve, one segment per frame.
 hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, const double* az_table, int G,
-                           const double* y, const unsigned* amask, const long long* seg, int F, double k, double ridge,
+                           const double* y, const unsigned* amask, const long long* seg, long long n, int F, double k,
+                           double ridge,
                            const double* bounds4, double* out, double* resid, double* pred);
 
 // K9: greedy association and wrapped-phase multi-start solve (rsl_wrap.hip).

@@ -71,7 +71,7 @@ RSL_DEV void vel_load(long long i0, long long e, const int* __restrict__ gidx, c
 __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az, const int* __restrict__ gidx,
                                                   const double* __restrict__ az_table, int G,
                                                   const double* __restrict__ y, const unsigned* __restrict__ amask,
-                                                  const long long* __restrict__ seg, double k, double ridge,
+                                                  const long long* __restrict__ seg, long long nmax, double k, double ridge,
                                                   double lx, double hx, double ly, double hy,
                                                   double* __restrict__ out, double* __restrict__ resid,
                                                   double* __restrict__ pred) {
@@ -85,7 +85,8 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
     __syncthreads();
   }
   const long f = blockIdx.x;
-  const long long b = seg[f], e = seg[f + 1];
+  // segment bounds clamped to the arrays' length (an overflowed capacity-sized list ends at its capacity)
+  const long long b = seg[f] < nmax ? seg[f] : nmax, e = seg[f + 1] < nmax ? seg[f + 1] : nmax;
   double n = 0, cc = 0, cs = 0, ss = 0, cy = 0, sy = 0, yy = 0;
   auto acc1 = [&](double w, double c, double s, double yi) {
     n += w;
@@ -204,11 +205,11 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
 }
 
 hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, const double* az_table, int G,
-                           const double* y, const unsigned* amask, const long long* seg, int F, double k, double ridge,
+                           const double* y, const unsigned* amask, const long long* seg, long long n, int F, double k, double ridge,
                            const double* bounds4, double* out, double* resid, double* pred) {
   if (F <= 0) return hipSuccess;
   const size_t lds = gidx ? sizeof(double) * 2 * (size_t)G : 0;
-  hipLaunchKernelGGL(k_velocity, dim3(F), dim3(512), lds, st, az, gidx, az_table, G, y, amask, seg, k, ridge,
+  hipLaunchKernelGGL(k_velocity, dim3(F), dim3(512), lds, st, az, gidx, az_table, G, y, amask, seg, n, k, ridge,
                      bounds4[0], bounds4[1], bounds4[2], bounds4[3], out, resid, pred);
   return hipGetLastError();
 }

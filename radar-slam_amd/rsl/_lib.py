@@ -49,8 +49,8 @@ SIGNATURES = {
     'rsl_cell_extras': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, c_longlong, c_double, _P, _P, _P, _P,
                                 _P, _P]),
     'rsl_confidence': (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, c_longlong, _P, _P, _P, _P]),
-    'rsl_velocity': (c_int, [_P, _P, _P, _P, c_int, _P, _P, _P, c_int, c_double, c_double, POINTER(c_double), _P,
-                             _P, _P]),
+    'rsl_velocity': (c_int, [_P, _P, _P, _P, c_int, _P, _P, _P, c_longlong, c_int, c_double, c_double,
+                             POINTER(c_double), _P, _P, _P]),
     'rsl_preprocess_rows': (c_int, [_P, _P, c_longlong, c_int, _P, c_int, _P]),
     'rsl_phase_model': (c_int, [_P, _P, _P, c_longlong, _P, c_double, _P, c_int, c_double, _P, _P, _P]),
     'rsl_associate': (c_int, [_P, _P, c_int, _P, c_int, c_double, _P, _P, _P]),

@@ -109,6 +109,9 @@ class RadarChain:
     def run_front(self, cube):
         """Memory-bound half: RDS + detection, offsets, peak / cell compaction (current stream)."""
         ctx, cfg = self.ctx, self.cfg
+        if self.F == 0:  # empty batch: only the (zeroed) bases
+            ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
+            return
         group = ctx.rds_detect(cube, self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds, work=self.work,
                                mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow,
                                dc_removal=cfg.dc_removal)
@@ -120,6 +123,8 @@ class RadarChain:
         """Compute-bound half: DoA scan (+ ESPRIT, phase) and the velocity solve, on run_front's lists."""
         ctx, cfg = self.ctx, self.cfg
         L = self.lists
+        if self.F == 0:
+            return
         if self.fused_doa:
             ctx.doa_extras(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
                            n_dev=self.ncell_dev, esprit_scale=self.esprit_scale, out_idx=self.gidx,
@@ -131,7 +136,8 @@ class RadarChain:
                             esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, bufs=self.ext)
         if velocity:
             ctx.velocity(None, self.ext['phase'], self.offs['cell_base'], k=self.k, ridge=cfg.ridge,
-                         bounds=cfg.bounds, amask=L['c_amask'], out=self.vel, gidx=self.gidx, az_table=self.az_table)
+                         bounds=cfg.bounds, amask=L['c_amask'], out=self.vel, gidx=self.gidx, az_table=self.az_table,
+                         n=self.cell_cap)
 
     def totals(self):
         eb = self.offs['entry_base'][self.F].item()

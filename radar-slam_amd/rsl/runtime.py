@@ -270,18 +270,19 @@ class Context:
 
     # -- a25-a29 ---------------------------------------------------------------------------------
     def velocity(self, az, y, seg, *, k: float, ridge: float = 0.0, bounds=(-50.0, 50.0, -50.0, 50.0),
-                 amask=None, want_resid=False, out=None, gidx=None, az_table=None):
+                 amask=None, want_resid=False, out=None, gidx=None, az_table=None, n=None):
+        """n: the per-target arrays' length (default len(y)); the segments in seg are clamped to it."""
         torch = self.torch
         F = int(seg.shape[0]) - 1
         o = out if out is not None else self.empty((max(F, 1), 8), torch.float64)
-        N = int(y.shape[0])
+        N = int(y.shape[0]) if n is None else min(int(n), int(y.shape[0]))
         G = int(az_table.shape[0]) if az_table is not None else 0
         resid = self.empty((max(N, 1),), torch.float64) if want_resid else None
         pred = self.empty((max(N, 1),), torch.float64) if want_resid else None
         b4 = (c_double * 4)(*[float(x) for x in bounds])
         self._bind()
         self.check(self.lib.rsl_velocity(self.h, _ptr(az), _ptr(gidx), _ptr(az_table), G, _ptr(y), _ptr(amask),
-                                         _ptr(seg), F, float(k), float(ridge), b4, _ptr(o), _ptr(resid), _ptr(pred)),
+                                         _ptr(seg), N, F, float(k), float(ridge), b4, _ptr(o), _ptr(resid), _ptr(pred)),
                    'rsl_velocity')
         return o, resid, pred
 
