@@ -16,6 +16,44 @@ namespace rsl {
 
 constexpr int kThreads = 256;
 
+// Global accesses with an optional non-temporal hint (`nt`: streamed once, not kept in L2 / MALL).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <bool NTH>
+RSL_DEV float4 ld16(const float4* p) {
+  if constexpr (NTH) {
+    return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p)));
+  } else {
+    return *p;
+  }
+}
+template <bool NTH>
+RSL_DEV void st16(float4* p, float4 x) {
+  if constexpr (NTH) {
+    f4v v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+  } else {
+    *p = x;
+  }
+}
+template <bool NTH>
+RSL_DEV float2 ld8(const float2* p) {
+  if constexpr (NTH) {
+    return __builtin_bit_cast(float2, __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
+  } else {
+    return *p;
+  }
+}
+template <bool NTH>
+RSL_DEV void st8(float2* p, float2 x) {
+  if constexpr (NTH) {
+    f2v v = {x.x, x.y};
+    __builtin_nontemporal_store(v, reinterpret_cast<f2v*>(p));
+  } else {
+    *p = x;
+  }
+}
+
 // Grid of a persistent kernel: resident workgroups only (occupancy x CUs), at most ntile.
 static long resident_grid(const void* kern, size_t lds, long ntile) {
   int nb = 0, dev = 0, ncu = 256;
@@ -113,7 +151,8 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // and issues the next tile's 16-B global loads into registers before running the current tile's LDS FFT, so
 // HBM latency overlaps the FFT instead of stalling every tile's load phase.  Requires even S with
 // rows_for(S) * S / 2 a multiple of the block size (every power-of-two S >= 16).
-template <int S, int CB, int DBG = 0>
+// CP (cache policy) bit 0: nt cube loads, bit 1: nt work stores, bit 2: masked loads (A/B)
+template <int S, int CB, int DBG = 0, int CP = 0>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
@@ -142,17 +181,26 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
     for (int q = 0; q < PF; ++q) {
       const int idx = tid + q * kThreads;
       const int r = idx / H;
-      nx[q] = (r < nrows) ? src4[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+      // unconditional (clamped) load, rows past nrows zeroed at consumption (a select on the loaded value here
+      // would wait for it); CP bit 2: the masked-load form
+      if constexpr ((CP & 4) != 0)
+        nx[q] = (r < nrows) ? src4[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+      else
+        nx[q] = ld16<(CP & 1) != 0>(src4 + (r < nrows ? idx : 0));
     }
   };
   long t = blockIdx.x;
   if (t < ntile) load(t);
   for (; t < ntile; t += gridDim.x) {
+    const int nrows_t = min(CB, C - (int)(t % ncb) * CB);
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int idx = tid + q * kThreads;
       const int r = idx / H, s2 = idx - r * H;
-      const float4 x = nx[q], tb = tab[q];
+      float4 x = nx[q];
+      const float4 tb = tab[q];
+      if constexpr ((CP & 4) == 0)
+        if (r >= nrows_t) x = make_float4(0.f, 0.f, 0.f, 0.f);
       buf[r * LD + lp(2 * s2)] = cmul(make_float2(x.x, x.y), make_float2(tb.x, tb.y));
       buf[r * LD + lp(2 * s2 + 1)] = cmul(make_float2(x.z, x.w), make_float2(tb.z, tb.w));
     }
@@ -173,7 +221,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
       const int r = idx / H, s2 = idx - r * H;
       if (r < nrows) {
         const float2 lo = buf[r * LD + lp(2 * s2)], hi = buf[r * LD + lp(2 * s2 + 1)];
-        dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);
+        if constexpr ((CP & 2) != 0)
+          st16<true>(dst4 + idx, make_float4(lo.x, lo.y, hi.x, hi.y));
+        else
+          dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);
       }
     }
     __syncthreads();  // buf is rewritten by the next tile
@@ -304,7 +355,7 @@ constexpr bool dd_reg_ok() {
   return C % 64 == 0 && KB % 8 == 0 && (C / 64) * (KB / 8) * 64 == NT && KB * (C / 64) <= 64;
 }
 
-template <int C, int KB, int NT, int DBG = 0>
+template <int C, int KB, int NT, int DBG = 0, int CP = 0>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
                                  int* __restrict__ row_count, float* __restrict__ dbmap,
@@ -326,7 +377,12 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   for (int r = 0; r < 10; ++r) {
     const float2 z = col[(rb + r) * LD];
     p[r] = cabs2(z);
-    if (r >= 1 && r <= 8) dst[(size_t)(r - 1) * C] = z;
+    if (r >= 1 && r <= 8) {
+      if constexpr ((CP & 2) != 0)
+        st8<true>(dst + (size_t)(r - 1) * C, z);
+      else
+        dst[(size_t)(r - 1) * C] = z;
+    }
   }
   float vm[8];
 #pragma unroll
@@ -403,7 +459,8 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-template <int C, int KB, int NT, bool PAD, int DBG = 0>
+// CP (cache policy) bit 0: nt interior loads, bit 1: nt RDS stores, bit 2: nt halo loads
+template <int C, int KB, int NT, bool PAD, int DBG = 0, int CP = 0>
 __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
                                                              float thr_f, int i_lo, int i_hi,
@@ -440,7 +497,12 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
     float2 ld[PI + PH];
     const float2* p = src + (unsigned)(cs * S + k0 + ri);
 #pragma unroll
-    for (int q = 0; q < PI; ++q) ld[q] = p[(unsigned)(q * CS * S)];
+    for (int q = 0; q < PI; ++q) {
+      if constexpr ((CP & 1) != 0)
+        ld[q] = ld8<true>(p + (unsigned)(q * CS * S));
+      else
+        ld[q] = p[(unsigned)(q * CS * S)];
+    }
     int kl = k0 - 1, kh = k0 + KB;  // halo range bins (periodic: reflect is applied in the detect stage)
     if (kl < 0) kl += S;
     if (kh >= S) kh -= S;
@@ -449,7 +511,10 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
       const int e = tid + h * NT;
       if ((2 * C) % NT == 0 || e < 2 * C) {
         const int side = e / C, c = e - side * C;
-        ld[PI + h] = src[(unsigned)(c * S + (side ? kh : kl))];
+        if constexpr ((CP & 4) != 0)
+          ld[PI + h] = ld8<true>(src + (unsigned)(c * S + (side ? kh : kl)));
+        else
+          ld[PI + h] = src[(unsigned)(c * S + (side ? kh : kl))];
       }
     }
 #pragma unroll
@@ -493,7 +558,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   __syncthreads();
   if constexpr (PAD && (DBG == 0 || DBG >= 4) && dd_reg_ok<C, KB, NT>()) {
     fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);
-    dd_tile_compute_reg<C, KB, NT, DBG>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi,
+    dd_tile_compute_reg<C, KB, NT, DBG, CP>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi,
                                    mask, row_count, dbmap, pk_pow);
   } else {
     dd_tile_compute<C, KB, NT, PAD, DBG>(buf, tws, S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap,
@@ -597,14 +662,25 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // 256 threads (a 320-thread block that runs each radix-8 stage of the 18-row KB-16 tile in one pass measured
   // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
   constexpr int NT = 256;
-  auto kern = pad ? k_doppler_detect<C, KB, NT, true> : k_doppler_detect<C, KB, NT, false>;
+  // nt RDS stores (the product output, not re-read by this stage; tools/cp_ab.py: 1.68 vs 1.70 ms per 1000 frames)
+  auto kern = pad ? k_doppler_detect<C, KB, NT, true, 0, 2> : k_doppler_detect<C, KB, NT, false>;
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (timing only: results are wrong)
     const int v = atoi(e);
-    if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1>;
-    if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2>;
-    if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3>;
-    if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4>;
-    if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5>;
+    if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, 2>;
+    if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2, 2>;
+    if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3, 2>;
+    if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4, 2>;
+    if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5, 2>;
+  }
+  if constexpr (C == 128 && KB == 16) {
+    if (const char* e = getenv("RSL_DD_CP")) {  // cache-policy variants (A/B tuning)
+      const int v = atoi(e);
+      if (v == 0) kern = k_doppler_detect<C, KB, NT, true, 0, 0>;
+      if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 0, 1>;
+      if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 0, 3>;
+      if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 0, 4>;
+      if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 0, 7>;
+    }
   }
   if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {
     const char* ep = getenv("RSL_DD_PERSIST");
@@ -671,9 +747,21 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       constexpr int CBX = decltype(cbc)::value;
       const long ntile = (long)F * A * ((C + CBX - 1) / CBX);
       const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CBX * lp_row(S));
-      auto kern = k_range_fft_p<S, CBX>;
+      // nt cube loads and nt work stores (both streamed once per batch; tools/cp_ab.py, tools/cpb.sh: 1.48-1.57 vs
+      // 1.57-1.64 ms per 1000 cfg2 frames in the pipelined bench)
+      auto kern = k_range_fft_p<S, CBX, 0, 3>;
       if (const char* e = getenv("RSL_RF_DBG"))  // ablation (timing only: results are wrong)
         if (atoi(e) == 1) kern = k_range_fft_p<S, CBX, 1>;
+      if constexpr (S == 512) {
+        if (const char* e = getenv("RSL_RF_CP")) {  // cache-policy variants (A/B tuning)
+          const int v = atoi(e);
+          if (v == 0) kern = k_range_fft_p<S, CBX, 0, 0>;
+          if (v == 1) kern = k_range_fft_p<S, CBX, 0, 1>;
+          if (v == 2) kern = k_range_fft_p<S, CBX, 0, 2>;
+          if (v == 4) kern = k_range_fft_p<S, CBX, 0, 4>;
+          if (v == 6) kern = k_range_fft_p<S, CBX, 0, 6>;
+        }
+      }
       const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile, table, tw,
                          dc, work);
