@@ -151,9 +151,13 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // and issues the next tile's 16-B global loads into registers before running the current tile's LDS FFT, so
 // HBM latency overlaps the FFT instead of stalling every tile's load phase.  Requires even S with
 // rows_for(S) * S / 2 a multiple of the block size (every power-of-two S >= 16).
-// CP (cache policy) bit 0: nt cube loads, bit 1: nt work stores, bit 2: masked loads (A/B)
-template <int S, int CB, int DBG = 0, int CP = 0>
-__global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
+// CP (cache policy) bit 0: nt cube loads, bit 1: nt work stores, bit 2: masked loads (A/B).
+// PD: tiles in flight per workgroup (1: the next tile's loads during this tile's FFT; 2: the next two, in two register
+// sets used in turn, registers capped for 3 waves per SIMD (9 dwords spilled); 3: as 2, uncapped, 2 waves per SIMD).
+// Measured (tools/rf_pd.py, tools/cpb.sh): depth 2 is faster before the plain Doppler kernel (1.55 vs 1.68 ms per 1000
+// cfg2 frames) but not in the chain (1.63 vs 1.63 ms; 178.9 vs 178.5 k frames/s), so depth 1 stays the default.
+template <int S, int CB, int DBG = 0, int CP = 0, int PD = 1>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PD == 2 ? 3 : 1))) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
                                                            float2* __restrict__ work) {
@@ -161,18 +165,22 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
   constexpr int H = S / 2;                 // float4 (2 complex) per row
   constexpr int PF = CB * H / kThreads;    // float4 per thread per tile
   static_assert((CB * H) % kThreads == 0, "tile must split evenly over the block");
+  static_assert(PD >= 1 && PD <= 3, "prefetch variant 1, 2 or 3");
+  constexpr int DEPTH = PD == 1 ? 1 : 2;
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + lp_row(S);
   const int tid = threadIdx.x;
   const int ncb = (C + CB - 1) / CB;
+  const long G = gridDim.x;
   for (int k = tid; k < S; k += kThreads) tws[lp(k)] = tw[k];
   const float4* tab4 = reinterpret_cast<const float4*>(table);
-  float4 tab[PF];
+  // the thread's table entries (one float4 when the block spans whole rows: every q hits the same samples)
+  constexpr int NTAB = (kThreads % H == 0) ? 1 : PF;
+  float4 tab[NTAB];
 #pragma unroll
-  for (int q = 0; q < PF; ++q) tab[q] = tab4[(tid + q * kThreads) % H];
-  float4 nx[PF];
-  auto load = [&](long t) {
+  for (int q = 0; q < NTAB; ++q) tab[q] = tab4[(tid + q * kThreads) % H];
+  auto load = [&](float4(&nx)[PF], long t) {
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
     const int nrows = min(CB, C - cb * CB);
@@ -189,31 +197,29 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
         nx[q] = ld16<(CP & 1) != 0>(src4 + (r < nrows ? idx : 0));
     }
   };
-  long t = blockIdx.x;
-  if (t < ntile) load(t);
-  for (; t < ntile; t += gridDim.x) {
-    const int nrows_t = min(CB, C - (int)(t % ncb) * CB);
+  // one tile: stage nx (x conj(ref) w) in LDS, refill nx with tile t + PD G, FFT, DC bin, store
+  auto body = [&](float4(&nx)[PF], long t) {
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    const int nrows = min(CB, C - cb * CB);
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int idx = tid + q * kThreads;
       const int r = idx / H, s2 = idx - r * H;
       float4 x = nx[q];
-      const float4 tb = tab[q];
+      const float4 tb = tab[NTAB == 1 ? 0 : q];
       if constexpr ((CP & 4) == 0)
-        if (r >= nrows_t) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r >= nrows) x = make_float4(0.f, 0.f, 0.f, 0.f);
       buf[r * LD + lp(2 * s2)] = cmul(make_float2(x.x, x.y), make_float2(tb.x, tb.y));
       buf[r * LD + lp(2 * s2 + 1)] = cmul(make_float2(x.z, x.w), make_float2(tb.z, tb.w));
     }
     __syncthreads();
-    if (t + gridDim.x < ntile) load(t + gridDim.x);  // in flight during the FFT below
+    if (t + DEPTH * G < ntile) load(nx, t + DEPTH * G);  // in flight during the FFT below (and the next PD - 1 tiles)
     if constexpr (DBG != 1) fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);  // DBG 1: no FFT (ablation)
     if (dc) {
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
       __syncthreads();
     }
-    const int cb = (int)(t % ncb);
-    const long fa = t / ncb;
-    const int nrows = min(CB, C - cb * CB);
     float4* dst4 = reinterpret_cast<float4*>(work + ((size_t)fa * C + cb * CB) * S);
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
@@ -228,6 +234,20 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
       }
     }
     __syncthreads();  // buf is rewritten by the next tile
+  };
+  long t = blockIdx.x;
+  if constexpr (PD == 1) {
+    float4 nx[PF];
+    if (t < ntile) load(nx, t);
+    for (; t < ntile; t += G) body(nx, t);
+  } else {
+    float4 na[PF], nb[PF];
+    if (t < ntile) load(na, t);
+    if (t + G < ntile) load(nb, t + G);
+    for (; t < ntile; t += 2 * G) {
+      body(na, t);
+      if (t + G < ntile) body(nb, t + G);
+    }
   }
 }
 
@@ -750,6 +770,11 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       // nt cube loads and nt work stores (both streamed once per batch; tools/cp_ab.py, tools/cpb.sh: 1.48-1.57 vs
       // 1.57-1.64 ms per 1000 cfg2 frames in the pipelined bench)
       auto kern = k_range_fft_p<S, CBX, 0, 3>;
+      if constexpr (S == 512) {
+        if (const char* e = getenv("RSL_RF_PD")) {  // two tiles in flight per workgroup (A/B)
+          if (atoi(e) == 2) kern = k_range_fft_p<S, CBX, 0, 3, 2>;
+        }
+      }
       if (const char* e = getenv("RSL_RF_DBG"))  // ablation (timing only: results are wrong)
         if (atoi(e) == 1) kern = k_range_fft_p<S, CBX, 1>;
       if constexpr (S == 512) {
