@@ -675,7 +675,9 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   const char* pe = getenv("RSL_DD_PAD");
   const bool pad = !pe || atoi(pe) != 0;
   // + the register body's exchange area (edge columns and ballots: 16 B per row per 64 columns)
-  const size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * ((pad ? lp_row(C) : C) | 1)) + (size_t)KB * (C / 64) * 16;
+  size_t lds = sizeof(float2) * (C + (size_t)(KB + 2) * ((pad ? lp_row(C) : C) | 1)) + (size_t)KB * (C / 64) * 16;
+  if (const char* e = getenv("RSL_DD_LDS"))  // LDS reserved per workgroup (fewer per CU: room for another kernel; A/B)
+    if ((size_t)atol(e) > lds) lds = (size_t)atol(e);
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
   // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
