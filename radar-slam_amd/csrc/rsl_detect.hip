@@ -249,19 +249,10 @@ RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
   return pre + x - v;
 }
 
-// Scalar store with an optional non-temporal hint (written once, read back by the host only).
-template <bool NTH, class T, class V>
-RSL_DEV void put(T* p, V v) {
-  const T x = (T)v;
-  if constexpr (NTH)
-    __builtin_nontemporal_store(x, p);
-  else
-    *p = x;
-}
-
-// NTE: nt stores of the entry arrays
-template <int W, int MAXA, bool NTE = false>
-__global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __restrict__ mask,
+// WPE: minimum waves per SIMD the register allocation must allow (0: unconstrained; A/B knob RSL_EMIT_WPE).
+// (Non-temporal entry stores were measured slower: 0.53 vs 0.48 ms per 1000 cfg2 frames.)
+template <int W, int MAXA, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void k_emit_block(const unsigned long long* __restrict__ mask,
                                                     const unsigned long long* __restrict__ umask,
                                                     const float* __restrict__ pk_pow, int pk_group, long long F,
                                                     int A, int S, int C, const int* __restrict__ entry_row_off,
@@ -377,11 +368,11 @@ __global__ __launch_bounds__(256) void k_emit_block(const unsigned long long* __
             const int tt = (int)(code >> 6), b = (int)(code & 63);
             const int ww = (int)((gw0 + tt) % W);
             const int ai = s_fi[tt];
-            put<NTE>(e_ant + e, ai >> 16);
-            put<NTE>(e_rbin + e, ai & 0xffff);
-            put<NTE>(e_dbin + e, ww * 64 + b);
-            put<NTE>(e_cell + e, s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull)));
-            if (e_pdb) put<NTE>(e_pdb + e, (double)(10.0f * log10f(pw[uu] + 1e-12f)));  // dechirp.py:235-236
+            e_ant[e] = ai >> 16;
+            e_rbin[e] = ai & 0xffff;
+            e_dbin[e] = ww * 64 + b;
+            e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
+            if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pw[uu] + 1e-12f));  // dechirp.py:235-236
           }
         }
       } else {
@@ -508,11 +499,12 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  const char* en = getenv("RSL_EMIT_NT");
-  const bool nte = en && atoi(en) != 0;
+  // registers capped for 7 waves per SIMD (72 VGPRs, no spill; 7 workgroups per CU as the LDS allows, instead of 6):
+  // emit 0.45-0.47 vs 0.46-0.48 ms per 1000 cfg2 frames (tools/cpb.sh); RSL_EMIT_WPE=0 for the unconstrained form
+  const char* ew = getenv("RSL_EMIT_WPE");
+  const int wpe = ew ? atoi(ew) : 7;
 #define GO(WW)                                                                                                   \
-  hipLaunchKernelGGL((A <= 8 ? (nte ? k_emit_block<WW, 8, true> : k_emit_block<WW, 8>)                           \
-                             : (nte ? k_emit_block<WW, 32, true> : k_emit_block<WW, 32>)),                       \
+  hipLaunchKernelGGL((A <= 8 ? (wpe == 7 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 8>) : k_emit_block<WW, 32>),  \
                      dim3(nb), dim3(256), 0, st, mask,                                                           \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
                      entry_cap, cell_cap, nbe, e_ant, e_rbin, e_dbin, e_cell, e_pdb, c_frame, c_rc, c_amask);

@@ -1,8 +1,6 @@
 # End-to-end bench A/B of one knob set (edit the variants; tools/cp_ab.py / rf_pd.py time the kernels alone)
 set -e
-for i in 1 2; do
+for i in 1 2 3; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/cpb_a_$i.json 2>/dev/null
-  RSL_DD_LDS=27648 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/cpb_b_$i.json 2>/dev/null
-  RSL_DD_LDS=27648 RSL_RF_BPC=2 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/cpb_c_$i.json 2>/dev/null
-  RSL_RF_BPC=2 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/cpb_d_$i.json 2>/dev/null
+  RSL_EMIT_WPE=7 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/cpb_b_$i.json 2>/dev/null
 done
