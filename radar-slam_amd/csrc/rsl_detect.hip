@@ -411,8 +411,11 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
                                                     const long long* __restrict__ cell_base, long long cell_cap,
                                                     int* __restrict__ c_frame, int* __restrict__ c_rc,
                                                     unsigned* __restrict__ c_amask) {
-  __shared__ unsigned pk[kCellCap];   // item code: (thread << 4) | bit within the thread's 16-bit slice
-  __shared__ unsigned pam[kCellCap];  // antenna mask of the item's cell
+  // item code (thread << 4) | bit within the thread's 16-bit slice (12 bits); for MAXA <= 16 the cell's antenna mask
+  // is packed above it (16 KiB of LDS instead of 32: 5 workgroups per CU instead of 4)
+  constexpr bool PACK = MAXA <= 16;
+  __shared__ unsigned pk[kCellCap];
+  __shared__ unsigned pam[PACK ? 1 : kCellCap];
   __shared__ int wsum[4];
   __shared__ long long s_first;
   const int t = threadIdx.x;
@@ -443,8 +446,12 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
       unsigned am = 0;
 #pragma unroll
       for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> bit) & 1ull) << aa;
-      pk[o] = ((unsigned)t << 4) | (unsigned)b;
-      pam[o] = am;
+      if constexpr (PACK) {
+        pk[o] = ((unsigned)t << 4) | (unsigned)b | (am << 12);
+      } else {
+        pk[o] = ((unsigned)t << 4) | (unsigned)b;
+        pam[o] = am;
+      }
       ++o;
     }
   }
@@ -454,14 +461,14 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
     const long long e = first + k;
     if (e < cell_cap) {
       const unsigned code = pk[k];
-      const int tt = (int)(code >> 4);
+      const int tt = (int)((code >> 4) & 0xffu);
       const long long g2 = gw0 + (tt >> 2);
       const long long rw = g2 / W;
       const int ww = (int)(g2 - rw * W);
       const long long ff = rw / S;
       c_frame[e] = (int)ff;
       c_rc[e] = (int)(rw - ff * S) * C + ww * 64 + 16 * (tt & 3) + (int)(code & 15);
-      c_amask[e] = pam[k];
+      c_amask[e] = PACK ? code >> 12 : pam[k];
     }
   }
 }
