@@ -29,7 +29,7 @@ METRIC = "radar frames/sec end-to-end, 8ch×128chirp×512 cube; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
-PROFILE = os.path.join(ROOT, 'profiles', 'r1h_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r1i_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
@@ -117,7 +117,7 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--frames-per-step', type=int, default=None,
-                    help='frames per GPU per step (default 1000 for cfg2, 100 for cfg5)')
+                    help='frames per GPU per step (default 2000 for cfg2, 100 for cfg5)')
     ap.add_argument('--config', choices=('cfg2', 'cfg5'), default='cfg2',
                     help='cfg2 = configs[2] (A8 C128 S512, the metric\'s workload); cfg5 = the configs[4] frame shape '
                          '(A16 C256 S1024), a second measurement, not the metric line')
@@ -153,7 +153,7 @@ def main():
     if args.config == 'cfg5':
         A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 100
     else:
-        A, C, S, Tc, F = 8, 128, 512, 51.2e-6, args.frames_per_step or 1000
+        A, C, S, Tc, F = 8, 128, 512, 51.2e-6, args.frames_per_step or 2000  # 5 steps = configs[2]'s 10 k frames
     cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
     ctx = rsl.get_context(local)
     NS = max(1, args.streams)

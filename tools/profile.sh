@@ -8,7 +8,7 @@ TAG=${1:-r1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timing --streams 1 --frames-per-step 1000"
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timing --streams 1 --frames-per-step 2000"
 # the kernel trace profiles the default bench command itself (its hipEvent averages are the ones reported)
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- python3 bench.py --no-cpu-baseline > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o p -- python3 $B > "$OUT/fetch.log" 2>&1
@@ -19,5 +19,6 @@ STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)
 mkdir -p profiles
 cp "$STATS" "profiles/${TAG}_kernel_stats.csv"
 python3 tools/pmc_summary.py --stats "$STATS" --fetch "$OUT/fetch" --write "$OUT/write" --extra "$OUT/busy" \
-  --out "profiles/${TAG}_pmc.json" --note "bench.py --steps 3 --warmup 1 (1000 cfg2 frames per launch); $(date -u)"
+  --out "profiles/${TAG}_pmc.json" --frames-per-launch 2000 \
+  --note "bench.py --steps 3 --warmup 1 (2000 cfg2 frames per launch); $(date -u)"
 cp "profiles/${TAG}_pmc.json" "profiles/${TAG}_kernel_stats.csv" "$OUT/"
