@@ -103,16 +103,20 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
                      void* entry_row_off, void* cell_row_off, void* scratch, void* entry_base, void* cell_base,
                      void* frame_counts, void* union_mask);
 
-/* Emit the peak entries (e_* arrays, i32; e_pdb f64 = per-entry power_db, nullable) and the unique cells
- * (c_frame i32, c_rc i32 = range_bin*C + doppler_bin, c_amask u32 = antennas with a peak there).
- * e_cell maps each entry to its cell.  Items beyond *_cap are dropped (compare the totals).
+/* Emit the peak entries and the unique cells (c_frame i32, c_rc i32 = range_bin*C + doppler_bin, c_amask u32 =
+ * antennas with a peak there).  An entry is e_coord u32 = antenna << 26 | range_bin << 13 | doppler_bin (the
+ * RSL_COORD_* macros; S, C <= 8192), e_cell i32 = its cell's list position, e_pdb f32 = power_db (nullable;
+ * dechirp.py:235-236, computed in fp32 from the fp32 RDS).  Items beyond *_cap are dropped (compare the totals).
  * With union_mask (from rsl_peak_offsets) and peak_pow (from rsl_detect / rsl_rds_detect, in the row grouping
  * peak_pow_group those report; 1 for rsl_detect) the RDS is not read (rds may be NULL); otherwise power_db is
  * recomputed from rds. */
 int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow,
                   int peak_pow_group, int F, int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
-                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
-                  void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
+                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_coord, void* e_cell,
+                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask);
+#define RSL_COORD_ANT(x) ((unsigned)(x) >> 26)
+#define RSL_COORD_RANGE(x) (((unsigned)(x) >> 13) & 0x1fffu)
+#define RSL_COORD_DOPPLER(x) ((unsigned)(x) & 0x1fffu)
 
 /* Host helper: MFMA operand tables of a steering matrix.  steer_c128 is the host [G][M] complex128
  * matrix of AngleEstimator.generate_steering_vector (angle_estimation.py:92-107) over the azimuth grid

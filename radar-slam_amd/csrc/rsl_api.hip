@@ -297,14 +297,15 @@ int rsl_peak_offsets(rsl_handle h, const void* mask, const void* row_count, int 
 
 int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* union_mask, const void* peak_pow,
                   int peak_pow_group, int F, int A, int S, int C, const void* entry_row_off, const void* cell_row_off, const void* entry_base,
-                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_ant, void* e_rbin,
-                  void* e_dbin, void* e_cell, void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
+                  const void* cell_base, long long entry_cap, long long cell_cap, void* e_coord, void* e_cell,
+                  void* e_pdb, void* c_frame, void* c_rc, void* c_amask) {
   if (!h) return RSL_ERR_INVALID;
-  if (F < 0 || A <= 0 || A > 32 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: bad shape");
+  if (F < 0 || A <= 0 || A > 32 || S <= 0 || C <= 0 || S > 8192 || C > 8192)
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: bad shape");
   if (F == 0) return RSL_OK;
   if (!mask || !entry_row_off || !cell_row_off || !entry_base || !cell_base)
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null pointer");
-  if ((entry_cap > 0 && (!e_ant || !e_rbin || !e_dbin || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
+  if ((entry_cap > 0 && (!e_coord || !e_cell)) || (cell_cap > 0 && (!c_frame || !c_rc || !c_amask)))
     return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: null output");
   const int W = (C + 63) / 64;
   if (peak_pow && (peak_pow_group < 1 || S % peak_pow_group != 0))
@@ -317,15 +318,15 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* u
                                        peak_pow_group, F, A, S, C,
                                        (const int*)entry_row_off, (const int*)cell_row_off,
                                        (const long long*)entry_base, (const long long*)cell_base, entry_cap, cell_cap,
-                                       (int*)e_ant, (int*)e_rbin, (int*)e_dbin, (int*)e_cell, (double*)e_pdb,
+                                       (unsigned*)e_coord, (int*)e_cell, (float*)e_pdb,
                                        (int*)c_frame, (int*)c_rc, (unsigned*)c_amask),
                      "emit2");
   if (!rds) return fail(h, RSL_ERR_INVALID, "rsl_peak_emit: rds needed without union_mask / peak_pow");
   return hip_check(h,
                    rsl::launch_emit(h->stream, (const float2*)rds, (const unsigned long long*)mask, F, A, S, C,
                                     (const int*)entry_row_off, (const int*)cell_row_off, (const long long*)entry_base,
-                                    (const long long*)cell_base, entry_cap, cell_cap, (int*)e_ant, (int*)e_rbin,
-                                    (int*)e_dbin, (int*)e_cell, (double*)e_pdb, (int*)c_frame, (int*)c_rc,
+                                    (const long long*)cell_base, entry_cap, cell_cap, (unsigned*)e_coord,
+                                    (int*)e_cell, (float*)e_pdb, (int*)c_frame, (int*)c_rc,
                                     (unsigned*)c_amask),
                    "emit");
 }

@@ -164,9 +164,9 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
                                               const int* __restrict__ entry_row_off, const int* __restrict__ cell_row_off,
                                               const long long* __restrict__ entry_base,
                                               const long long* __restrict__ cell_base, long long entry_cap,
-                                              long long cell_cap, int* __restrict__ e_ant, int* __restrict__ e_rbin,
-                                              int* __restrict__ e_dbin, int* __restrict__ e_cell,
-                                              double* __restrict__ e_pdb, int* __restrict__ c_frame,
+                                              long long cell_cap, unsigned* __restrict__ e_coord,
+                                              int* __restrict__ e_cell, float* __restrict__ e_pdb,
+                                              int* __restrict__ c_frame,
                                               int* __restrict__ c_rc, unsigned* __restrict__ c_amask) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // f * S + i
   if (row >= (long)F * S) return;
@@ -196,13 +196,11 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
         long long e = e0 + entry_row_off[(size_t)f * A * S + (size_t)a * S + i] + __popcll(m & lt);
         for (int ww = 0; ww < w; ++ww) e += __popcll(mrow[ww]);
         if (e < entry_cap) {
-          e_ant[e] = a;
-          e_rbin[e] = i;
-          e_dbin[e] = j;
+          e_coord[e] = ((unsigned)a << 26) | ((unsigned)i << 13) | (unsigned)j;
           e_cell[e] = (int)c;
           if (e_pdb) {
             const float p = cabs2(rf[((size_t)a * S + i) * C + j]);
-            e_pdb[e] = 10.0 * log10((double)p + 1e-12);
+            e_pdb[e] = (float)(10.0 * log10((double)p + 1e-12));
           }
         }
       }
@@ -259,9 +257,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
                                                     const int* __restrict__ cell_row_off,
                                                     const long long* __restrict__ entry_base,
                                                     const long long* __restrict__ cell_base, long long entry_cap,
-                                                    long long cell_cap, long long nblk_e, int* __restrict__ e_ant,
-                                                    int* __restrict__ e_rbin, int* __restrict__ e_dbin,
-                                                    int* __restrict__ e_cell, double* __restrict__ e_pdb,
+                                                    long long cell_cap, long long nblk_e,
+                                                    unsigned* __restrict__ e_coord, int* __restrict__ e_cell,
+                                                    float* __restrict__ e_pdb,
                                                     int* __restrict__ c_frame, int* __restrict__ c_rc,
                                                     unsigned* __restrict__ c_amask) {
   static_assert(64 % W == 0, "a mask row must lie within one wave");
@@ -368,11 +366,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
             const int tt = (int)(code >> 6), b = (int)(code & 63);
             const int ww = (int)((gw0 + tt) % W);
             const int ai = s_fi[tt];
-            e_ant[e] = ai >> 16;
-            e_rbin[e] = ai & 0xffff;
-            e_dbin[e] = ww * 64 + b;
+            e_coord[e] = ((unsigned)(ai >> 16) << 26) | ((unsigned)(ai & 0xffff) << 13) | (unsigned)(ww * 64 + b);
             e_cell[e] = s_cw[tt] + __popcll(s_u[tt] & ((1ull << b) - 1ull));
-            if (e_pdb) e_pdb[e] = (double)(10.0f * log10f(pw[uu] + 1e-12f));  // dechirp.py:235-236
+            if (e_pdb) e_pdb[e] = 10.0f * log10f(pw[uu] + 1e-12f);  // dechirp.py:235-236
           }
         }
       } else {
@@ -476,8 +472,8 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
 hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
                         const float* pk_pow, int pk_group, int F, int A, int S, int C, const int* entry_row_off,
                         const int* cell_row_off, const long long* entry_base, const long long* cell_base,
-                        long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
-                        double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
+                        long long entry_cap, long long cell_cap, unsigned* e_coord, int* e_cell, float* e_pdb,
+                        int* c_frame, int* c_rc, unsigned* c_amask) {
   if (F <= 0) return hipSuccess;
   if (A > 32) return hipErrorInvalidValue;
   const int W = (C + 63) / 64;
@@ -514,7 +510,7 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   hipLaunchKernelGGL((A <= 8 ? (wpe == 7 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 8>) : k_emit_block<WW, 32>),  \
                      dim3(nb), dim3(256), 0, st, mask,                                                           \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
-                     entry_cap, cell_cap, nbe, e_ant, e_rbin, e_dbin, e_cell, e_pdb, c_frame, c_rc, c_amask);
+                     entry_cap, cell_cap, nbe, e_coord, e_cell, e_pdb, c_frame, c_rc, c_amask);
   switch (W) {
     case 1: GO(1) break;
     case 2: GO(2) break;
@@ -555,13 +551,13 @@ hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const 
 
 hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long long* mask, int F, int A, int S, int C,
                        const int* entry_row_off, const int* cell_row_off, const long long* entry_base,
-                       const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
-                       int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
+                       const long long* cell_base, long long entry_cap, long long cell_cap, unsigned* e_coord,
+                       int* e_cell, float* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask) {
   if (F <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
   const long rows = (long)F * S;
   hipLaunchKernelGGL(k_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, rds, mask, F, A, S, C, W,
-                     entry_row_off, cell_row_off, entry_base, cell_base, entry_cap, cell_cap, e_ant, e_rbin, e_dbin,
+                     entry_row_off, cell_row_off, entry_base, cell_base, entry_cap, cell_cap, e_coord,
                      e_cell, e_pdb, c_frame, c_rc, c_amask);
   return hipGetLastError();
 }

@@ -48,16 +48,16 @@ hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const 
 // Emit compacted entries and cells in reference order.
 hipError_t launch_emit(hipStream_t st, const float2* rds, const unsigned long long* mask, int F, int A, int S, int C,
                        const int* entry_row_off, const int* cell_row_off, const long long* entry_base,
-                       const long long* cell_base, long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin,
-                       int* e_dbin, int* e_cell, double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
+                       const long long* cell_base, long long entry_cap, long long cell_cap, unsigned* e_coord,
+                       int* e_cell, float* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
 
 // Emit from group-compact peak powers (pk_group rows per group, 1 = row-compact) and union masks (no RDS read);
 // W = ceil(C/64) must be a power of two <= 64.
 hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const unsigned long long* umask,
                         const float* pk_pow, int pk_group, int F, int A, int S, int C, const int* entry_row_off,
                         const int* cell_row_off, const long long* entry_base, const long long* cell_base,
-                        long long entry_cap, long long cell_cap, int* e_ant, int* e_rbin, int* e_dbin, int* e_cell,
-                        double* e_pdb, int* c_frame, int* c_rc, unsigned* c_amask);
+                        long long entry_cap, long long cell_cap, unsigned* e_coord, int* e_cell, float* e_pdb,
+                        int* c_frame, int* c_rc, unsigned* c_amask);
 // K5: steering scan on MFMA (f32 16x16x4), argmax; optional spectrum.
 hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,

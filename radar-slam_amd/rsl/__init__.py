@@ -7,7 +7,7 @@ Layers: ``_lib`` (C ABI, include/rsl.h) -> ``runtime.Context`` (device buffers, 
 the ``src`` package next to this one (``src.radar_signal.dechirp.SignalPreprocessor`` ...).
 """
 from ._lib import LIB_PATH, load  # noqa: F401
-from .runtime import Context, get_context  # noqa: F401
+from .runtime import Context, get_context, unpack_coord  # noqa: F401
 from .chain import ChainConfig, RadarChain  # noqa: F401
 from .traj import TrajectoryReducer  # noqa: F401
 from .synth import SyntheticCubes  # noqa: F401

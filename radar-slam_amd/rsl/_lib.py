@@ -39,7 +39,7 @@ SIGNATURES = {
     'rsl_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_int, c_int, _P, _P, _P, _P]),
     'rsl_peak_offsets': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P]),
     'rsl_peak_emit': (c_int, [_P, _P, _P, _P, _P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_longlong,
-                              c_longlong, _P, _P, _P, _P, _P, _P, _P, _P]),
+                              c_longlong, _P, _P, _P, _P, _P, _P]),
     'rsl_steer_table_floats': (c_longlong, [c_int, c_int]),
     'rsl_steer_table_build': (c_int, [POINTER(c_double), c_int, c_int, POINTER(c_float), POINTER(c_int),
                                       POINTER(c_int)]),

@@ -17,7 +17,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib, tables
-from .runtime import Context, get_context
+from .runtime import Context, get_context, unpack_coord
 
 C_LIGHT = 3e8
 
@@ -91,8 +91,7 @@ class RadarChain:
                          cell_base=e((F + 1,), torch.int64), frame_counts=e((2 * F,), torch.int64),
                          union_mask=e((F, S, W), torch.int64))
         ec, cc = self.entry_cap, self.cell_cap
-        self.lists = dict(e_ant=e((ec,), torch.int32), e_rbin=e((ec,), torch.int32), e_dbin=e((ec,), torch.int32),
-                          e_cell=e((ec,), torch.int32), e_pdb=e((ec,), torch.float64),
+        self.lists = dict(e_coord=e((ec,), torch.int32), e_cell=e((ec,), torch.int32), e_pdb=e((ec,), torch.float32),
                           c_frame=e((cc,), torch.int32), c_rc=e((cc,), torch.int32), c_amask=e((cc,), torch.int32))
         self.gidx = e((cc,), torch.int32)
         self.ext = dict(esprit=e((cc,), torch.float64), phase=e((cc,), torch.float64), az=e((cc,), torch.float64))
@@ -152,8 +151,8 @@ class RadarChain:
         L = self.lists
         h = lambda t, n: t[:n].cpu().numpy()
         return dict(entry_base=self.offs['entry_base'].cpu().numpy(), cell_base=self.offs['cell_base'].cpu().numpy(),
-                    e_ant=h(L['e_ant'], ne), e_rbin=h(L['e_rbin'], ne), e_dbin=h(L['e_dbin'], ne),
-                    e_cell=h(L['e_cell'], ne), e_pdb=h(L['e_pdb'], ne), c_frame=h(L['c_frame'], nc),
+                    **dict(zip(('e_ant', 'e_rbin', 'e_dbin'), unpack_coord(h(L['e_coord'], ne)))),
+                    e_cell=h(L['e_cell'], ne), e_pdb=h(L['e_pdb'], ne).astype(np.float64), c_frame=h(L['c_frame'], nc),
                     c_rc=h(L['c_rc'], nc), c_amask=h(L['c_amask'], nc), gidx=h(self.gidx, nc),
                     esprit=h(self.ext['esprit'], nc), phase=h(self.ext['phase'], nc),
                     az=np.radians(self.grid)[h(self.gidx, nc)],

@@ -13,7 +13,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib, tables
-from .runtime import Context, get_context
+from .runtime import Context, get_context, unpack_coord
 
 
 def _ctx(ctx: Optional[Context]) -> Context:
@@ -94,8 +94,9 @@ def detect_peaks(rds, *, threshold_db=-20.0, i_lo=0, i_hi=1 << 30, want_db=True,
     ne = int(offs['entry_base'][F].item())
     nc = int(offs['cell_base'][F].item())
     lists = c.emit(d, mask, offs, ne, nc, want_pdb=True)
-    res = dict(antenna=to_host(lists['e_ant'][:ne]).astype(np.int64), range_bin=to_host(lists['e_rbin'][:ne]).astype(np.int64),
-               doppler_bin=to_host(lists['e_dbin'][:ne]).astype(np.int64), power_db=to_host(lists['e_pdb'][:ne]),
+    ant, rbin, dbin = unpack_coord(to_host(lists['e_coord'][:ne]))
+    res = dict(antenna=ant.astype(np.int64), range_bin=rbin.astype(np.int64), doppler_bin=dbin.astype(np.int64),
+               power_db=to_host(lists['e_pdb'][:ne], np.float64),
                entry_base=to_host(offs['entry_base']), cells=nc)
     if want_db:
         res['power_spectrum_db'] = to_host(db, np.float64)

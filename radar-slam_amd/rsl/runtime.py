@@ -19,6 +19,12 @@ from . import tables
 _P = c_void_p
 
 
+def unpack_coord(coord: np.ndarray):
+    """Host unpack of the emit's packed entries (include/rsl.h RSL_COORD_*): antenna, range_bin, doppler_bin."""
+    u = np.asarray(coord).view(np.uint32)
+    return ((u >> 26).astype(np.int32), ((u >> 13) & 0x1fff).astype(np.int32), (u & 0x1fff).astype(np.int32))
+
+
 def _ptr(t) -> Optional[c_void_p]:
     if t is None:
         return None
@@ -170,9 +176,9 @@ class Context:
         def get(name, n, dt):
             t = b.get(name)
             return t if t is not None else self.empty((max(n, 1),), dt)
-        e_ant, e_r, e_d, e_c = (get('e_ant', entry_cap, torch.int32), get('e_rbin', entry_cap, torch.int32),
-                                get('e_dbin', entry_cap, torch.int32), get('e_cell', entry_cap, torch.int32))
-        e_pdb = get('e_pdb', entry_cap, torch.float64) if want_pdb else None
+        # e_coord = antenna << 26 | range_bin << 13 | doppler_bin (u32 bits in an int32 tensor; unpack_coord)
+        e_co, e_c = get('e_coord', entry_cap, torch.int32), get('e_cell', entry_cap, torch.int32)
+        e_pdb = get('e_pdb', entry_cap, torch.float32) if want_pdb else None
         c_f, c_rc, c_am = (get('c_frame', cell_cap, torch.int32), get('c_rc', cell_cap, torch.int32),
                            get('c_amask', cell_cap, torch.int32))
         self._bind()
@@ -180,11 +186,10 @@ class Context:
                                           _ptr(peak_pow), int(peak_pow_group), F, A, S, C,
                                           _ptr(offs['entry_row_off']),
                                           _ptr(offs['cell_row_off']), _ptr(offs['entry_base']),
-                                          _ptr(offs['cell_base']), int(entry_cap), int(cell_cap), _ptr(e_ant),
-                                          _ptr(e_r), _ptr(e_d), _ptr(e_c), _ptr(e_pdb), _ptr(c_f), _ptr(c_rc),
-                                          _ptr(c_am)), 'rsl_peak_emit')
-        return dict(e_ant=e_ant, e_rbin=e_r, e_dbin=e_d, e_cell=e_c, e_pdb=e_pdb, c_frame=c_f, c_rc=c_rc,
-                    c_amask=c_am)
+                                          _ptr(offs['cell_base']), int(entry_cap), int(cell_cap), _ptr(e_co),
+                                          _ptr(e_c), _ptr(e_pdb), _ptr(c_f), _ptr(c_rc), _ptr(c_am)),
+                   'rsl_peak_emit')
+        return dict(e_coord=e_co, e_cell=e_c, e_pdb=e_pdb, c_frame=c_f, c_rc=c_rc, c_amask=c_am)
 
     # -- steering tables -------------------------------------------------------------------------
     def steering(self, steer_c128: np.ndarray):
