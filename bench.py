@@ -316,7 +316,7 @@ def main():
         line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
         if ks:
             line["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed on rank 0 at N = 1 only
         try:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         except Exception as e:  # the baseline is reported, never the target
