@@ -181,11 +181,12 @@ RSL_DEV float tile_max(const floatx16& a) {
 // Record-tile copy for the lanes that set a new record: 8 v_pk_mov_b32 (64-bit pairs) under the branch's exec mask
 // instead of 16 v_cndmask_b32 on every tile.  Volatile asm also keeps the compiler from speculating the branch into
 // per-value selects.
+template <int NCOPY = 8>  // NCOPY < 8: ablation (timing only)
 RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
   typedef double doublex8 __attribute__((ext_vector_type(8)));
   const doublex8 s = __builtin_bit_cast(doublex8, src);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,1]" : "=v"(dst[k]) : "v"(s[k]));
+  for (int k = 0; k < NCOPY; ++k) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,1]" : "=v"(dst[k]) : "v"(s[k]));
 }
 
 // Exact fp64 scan of one cell (MUSIC near-degenerate path): key = P if M - P > 1e-12 else -1, first index.
@@ -394,12 +395,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
       if (m0 > best0) {
         best0 = m0;
         bt0 = t;
-        if constexpr (DBG != 1) copy_tile(sv0, acc0);
+        if constexpr (DBG == 7) copy_tile<1>(sv0, acc0);
+        else if constexpr (DBG != 1) copy_tile(sv0, acc0);
       }
       if (m1 > best1) {
         best1 = m1;
         bt1 = t;
-        if constexpr (DBG != 1) copy_tile(sv1, acc1);
+        if constexpr (DBG == 7) copy_tile<1>(sv1, acc1);
+        else if constexpr (DBG != 1) copy_tile(sv1, acc1);
       }
     };
     {
@@ -469,6 +472,7 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 2) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 2, 12>;
         if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3, 12>;
         if (v == 4) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 4, 12>;
+        if (v == 7) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 7, 12>;
       }
     }
   }

@@ -1,5 +1,5 @@
 """Time the DoA kernel's ablation variants (RSL_DOA_DBG=0..4) on one cfg2 batch: 1 = no record-tile copies,
-2 = no MFMA, 3 = no signature loads, 4 = no Toeplitz operand math.  Results are wrong by construction for 1-4."""
+2 = no MFMA, 3 = no signature loads, 4 = no Toeplitz operand math, 7 = one of the eight record-tile copies.  Results are wrong by construction for 1-4."""
 import os, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, 'radar-slam_amd'), ROOT]
@@ -15,7 +15,7 @@ torch.cuda.synchronize()
 L = ch.lists
 res = {}
 for rnd in range(2):
-    for v in ['0', '1', '2', '3', '4']:
+    for v in ['0', '1', '2', '3', '4', '7']:
         os.environ['RSL_DOA_DBG'] = v
         idx = torch.empty_like(ch.gidx)
         run = lambda: ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, 1, n=ch.cell_cap, n_dev=ch.ncell_dev, out_idx=idx)
