@@ -422,6 +422,7 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   __syncthreads();
   unsigned long long* wb = reinterpret_cast<unsigned long long*>(xch + KB * 2 * NCH);  // [KB][NCH] ballots
   bool pkv[8];
+  unsigned long long bal[8];  // this wave's ballot word of each of its rows (wave-uniform)
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) {
     float l = __shfl_up(vm[rr], 1), r = __shfl_down(vm[rr], 1);
@@ -433,29 +434,29 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
     const bool pk = (i >= i_lo && i <= i_hi) && (pc > thr_f) && (pc >= m);
     pkv[rr] = pk;
     const unsigned long long b = __ballot(pk);
+    bal[rr] = b;
     if (lane == 0) wb[(rb + rr) * NCH + ch] = b;
     if (dbmap) dbmap[((size_t)fa * S + i) * C + j] = 10.f * log10f(pc + 1e-12f);
   }
   __syncthreads();
-  // peak powers compact over the tile's KB rows (one contiguous run from the tile's first row slot): the peaks
-  // of the rows before this wave's first row, then row by row
-  // (the tile's KB * NCH <= 64 ballot words: one per lane, summed across the wave instead of a serial LDS loop)
-  int pre = lane < rb * NCH ? __popcll(wb[lane]) : 0;
+  // peak powers compact over the tile's KB rows (one contiguous run from the tile's first row slot): an exclusive
+  // scan of the tile's KB * NCH <= 64 ballot-word popcounts (one word per lane) gives every word's offset; each row
+  // reads its word's offset with one v_readlane (the word index is wave-uniform) and ranks its lanes in its ballot
+  const unsigned long long myw = lane < KB * NCH ? wb[lane] : 0ull;
+  const int cw = __popcll(myw);
+  int incl = cw;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) pre += __shfl_xor(pre, off);
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const int v = __shfl_up(incl, dd);
+    if (lane >= dd) incl += v;
+  }
+  const int excl = incl - cw;
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
+  const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) {
-    int off = pre, cnt = 0;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int pc = __popcll(wb[(rb + rr) * NCH + c]);
-      off += c < ch ? pc : 0;
-      cnt += pc;
-    }
-    pre += cnt;
-    const unsigned long long b = wb[(rb + rr) * NCH + ch];
-    if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(b & ((1ull << lane) - 1ull))] = p[rr + 1];
+    const int off = __builtin_amdgcn_readlane(excl, (rb + rr) * NCH + ch);
+    if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(bal[rr] & lt)] = p[rr + 1];
   }
   // the tile's mask words and row counts from the ballots in LDS, one coalesced store each (the tile's shifted rows
   // i0 .. i0 + KB - 1 are contiguous), instead of single-lane stores per row and wave
