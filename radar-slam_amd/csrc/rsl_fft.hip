@@ -453,10 +453,25 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   const int excl = incl - cw;
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
   const unsigned long long lt = (1ull << lane) - 1ull;
+  if constexpr ((CP & 8) != 0) {
+    // CP bit 3: stage the tile's compacted peak powers in the (now dead) LDS tile, then one block-wide contiguous
+    // store of the whole run instead of 8 partial-line stores per wave
+    float* stg = reinterpret_cast<float*>(const_cast<float2*>(buf));
+    const int total = __builtin_amdgcn_readlane(incl, 63);
 #pragma unroll
-  for (int rr = 0; rr < 8; ++rr) {
-    const int off = __builtin_amdgcn_readlane(excl, (rb + rr) * NCH + ch);
-    if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(bal[rr] & lt)] = p[rr + 1];
+    for (int rr = 0; rr < 8; ++rr) {
+      const int off = __builtin_amdgcn_readlane(excl, (rb + rr) * NCH + ch);
+      if (pkv[rr]) stg[off + __popcll(bal[rr] & lt)] = p[rr + 1];
+    }
+    __syncthreads();
+    if (DBG != 4 && tile_pk)
+      for (int k = tid; k < total; k += NT) tile_pk[k] = stg[k];
+  } else {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int off = __builtin_amdgcn_readlane(excl, (rb + rr) * NCH + ch);
+      if (DBG != 4 && tile_pk && pkv[rr]) tile_pk[off + __popcll(bal[rr] & lt)] = p[rr + 1];
+    }
   }
   // the tile's mask words and row counts from the ballots in LDS, one coalesced store each (the tile's shifted rows
   // i0 .. i0 + KB - 1 are contiguous), instead of single-lane stores per row and wave
@@ -685,24 +700,27 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // 256 threads (a 320-thread block that runs each radix-8 stage of the 18-row KB-16 tile in one pass measured
   // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
   constexpr int NT = 256;
-  // nt RDS stores (the product output, not re-read by this stage; tools/cp_ab.py: 1.68 vs 1.70 ms per 1000 frames)
-  auto kern = pad ? k_doppler_detect<C, KB, NT, true, 0, 2> : k_doppler_detect<C, KB, NT, false>;
+  // nt RDS stores (the product output, not re-read by this stage; tools/cp_ab.py: 1.68 vs 1.70 ms per 1000 frames);
+  // peak powers staged in LDS and stored block-wide (tools/pkb.sh: 187.2-188.5 k vs 184.1-185.2 k frames/s)
+  auto kern = pad ? k_doppler_detect<C, KB, NT, true, 0, 10> : k_doppler_detect<C, KB, NT, false>;
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (timing only: results are wrong)
     const int v = atoi(e);
-    if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, 2>;
-    if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2, 2>;
-    if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3, 2>;
-    if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4, 2>;
-    if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5, 2>;
+    if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, 10>;
+    if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 2, 10>;
+    if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3, 10>;
+    if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4, 10>;
+    if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5, 10>;
   }
   if constexpr (C == 128 && KB == 16) {
     if (const char* e = getenv("RSL_DD_CP")) {  // cache-policy variants (A/B tuning)
       const int v = atoi(e);
       if (v == 0) kern = k_doppler_detect<C, KB, NT, true, 0, 0>;
       if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 0, 1>;
+      if (v == 2) kern = k_doppler_detect<C, KB, NT, true, 0, 2>;
       if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 0, 3>;
       if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 0, 4>;
       if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 0, 7>;
+      if (v == 10) kern = k_doppler_detect<C, KB, NT, true, 0, 10>;
     }
   }
   if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {
