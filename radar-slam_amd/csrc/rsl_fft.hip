@@ -6,6 +6,7 @@
 // DC removal is folded into the range FFT: FFT(y - mean y)[k] = FFT(y)[k] for k != 0 and 0 for k = 0,
 // so the kernel zeroes range bin 0 instead of reducing a mean (exact in real arithmetic).
 // conj(ref)*w is precomputed on the host in fp64 (the chirp phase reaches 2.5e7 rad) and passed as a c64 table.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -15,6 +16,12 @@
 namespace rsl {
 
 constexpr int kThreads = 256;
+
+// K1 work queues (RSL_RF_DYN): per launch slot, 8 per-XCD dequeue heads and 8 exit counters, each on its own 128-B
+// line. The last workgroup of an XCD to leave resets its pair, so a slot is clean for its next launch; the host
+// hands slots round-robin, so up to kRfSlots K1 launches may be in flight at once (on any streams).
+constexpr int kRfSlots = 8;
+__device__ unsigned g_rf_q[kRfSlots][2][8][32];
 
 // Global accesses with an optional non-temporal hint (`nt`: streamed once, not kept in L2 / MALL).
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -156,17 +163,16 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // sets used in turn, registers capped for 3 waves per SIMD (9 dwords spilled); 3: as 2, uncapped, 2 waves per SIMD).
 // Measured (tools/rf_pd.py, tools/cpb.sh): depth 2 is faster before the plain Doppler kernel (1.55 vs 1.68 ms per 1000
 // cfg2 frames) but not in the chain (1.63 vs 1.63 ms; 178.9 vs 178.5 k frames/s), so depth 1 stays the default.
-template <int S, int CB, int DBG = 0, int CP = 0, int PD = 1>
+template <int S, int CB, int DBG = 0, int CP = 0, int PD = 1, bool DYN = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PD == 2 ? 3 : 1))) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
-                                                           float2* __restrict__ work) {
+                                                           float2* __restrict__ work, int slot) {
   constexpr int LD = lp_row(S);
   constexpr int H = S / 2;                 // float4 (2 complex) per row
   constexpr int PF = CB * H / kThreads;    // float4 per thread per tile
   static_assert((CB * H) % kThreads == 0, "tile must split evenly over the block");
   static_assert(PD >= 1 && PD <= 3, "prefetch variant 1, 2 or 3");
-  constexpr int DEPTH = PD == 1 ? 1 : 2;
   extern __shared__ float2 sm[];
   float2* tws = sm;
   float2* buf = sm + lp_row(S);
@@ -198,7 +204,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PD == 
     }
   };
   // one tile: stage nx (x conj(ref) w) in LDS, refill nx with tile t + PD G, FFT, DC bin, store
-  auto body = [&](float4(&nx)[PF], long t) {
+  // DYN: workgroup b serves XCD x = b % 8 (dispatch order) and walks that XCD's tile range [lo, hi): its first two
+  // tiles are static, every later one comes from the XCD's dequeue head, claimed one tile ahead (the atomic returns
+  // during a whole tile), so workgroups that start late (CUs held by a concurrent kernel) take fewer tiles
+  __shared__ long s_nn;
+  const int xcd = blockIdx.x & 7;
+  const long gx = (G - xcd + 7) / 8;
+  const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
+  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  auto body = [&](float4(&nx)[PF], long t, long tn) {
+    unsigned claim = 0;
+    if (DYN && tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
     const int nrows = min(CB, C - cb * CB);
@@ -214,7 +230,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PD == 
       buf[r * LD + lp(2 * s2 + 1)] = cmul(make_float2(x.z, x.w), make_float2(tb.z, tb.w));
     }
     __syncthreads();
-    if (t + DEPTH * G < ntile) load(nx, t + DEPTH * G);  // in flight during the FFT below (and the next PD - 1 tiles)
+    if (tn < hi) load(nx, tn);  // in flight during the FFT below (and the next PD - 1 tiles)
     if constexpr (DBG != 1) fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);  // DBG 1: no FFT (ablation)
     if (dc) {
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
@@ -233,20 +249,38 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PD == 
           dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);
       }
     }
+    if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
     __syncthreads();  // buf is rewritten by the next tile
   };
+  if constexpr (DYN) {
+    static_assert(PD == 1, "dequeue variant: one tile in flight");
+    long t = lo + (blockIdx.x >> 3), tn = t + gx;
+    float4 nx[PF];
+    if (t < hi) load(nx, t);
+    while (t < hi) {
+      body(nx, t, tn);
+      t = tn;
+      tn = s_nn;  // written before body's last barrier, rewritten only after the next body's first one
+    }
+    // every dequeue of this workgroup has returned: the XCD's last leaver resets the slot for its next launch
+    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+      atomicExch(head, 0u);
+      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+    }
+    return;
+  }
   long t = blockIdx.x;
   if constexpr (PD == 1) {
     float4 nx[PF];
     if (t < ntile) load(nx, t);
-    for (; t < ntile; t += G) body(nx, t);
+    for (; t < ntile; t += G) body(nx, t, t + G);
   } else {
     float4 na[PF], nb[PF];
     if (t < ntile) load(na, t);
     if (t + G < ntile) load(nb, t + G);
     for (; t < ntile; t += 2 * G) {
-      body(na, t);
-      if (t + G < ntile) body(nb, t + G);
+      body(na, t, t + 2 * G);
+      if (t + G < ntile) body(nb, t + G, t + 3 * G);
     }
   }
 }
@@ -808,9 +842,20 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
           if (v == 6) kern = k_range_fft_p<S, CBX, 0, 6>;
         }
       }
-      const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
+      long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
+      int slot = 0;
+      // per-XCD dequeue of tiles (every XCD needs a workgroup; RSL_RF_DYN=0: the static walk): tools/dyn.sh, one call,
+      // K1 alone 1.499 vs 1.667 ms per 1000 cfg2 frames, outputs bit-identical; bench 187.8-189.0 vs 186.9-188.7 k
+      {
+        const char* e = getenv("RSL_RF_DYN");
+        if ((!e || atoi(e) != 0) && nblk >= 8 && !getenv("RSL_RF_DBG") && !getenv("RSL_RF_PD") && !getenv("RSL_RF_CP")) {
+          kern = k_range_fft_p<S, CBX, 0, 3, 1, true>;
+          static std::atomic<int> next_slot{0};
+          slot = next_slot.fetch_add(1) % kRfSlots;
+        }
+      }
       hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile, table, tw,
-                         dc, work);
+                         dc, work, slot);
       return hipGetLastError();
     };
     if constexpr (S == 512) {  // RSL_RF_CB: chirp rows per tile (4 / 8 / 16) for tuning
