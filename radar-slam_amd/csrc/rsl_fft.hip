@@ -427,11 +427,26 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   float p[10];
   const float2* col = buf + lp(d);
   float2* dst = rds + ((size_t)fa * S + i0 + rb) * C + j;
+  float2 zp = make_float2(0.f, 0.f);  // CP bit 4: the first row of the current row pair
+  const bool odd = (lane & 1) != 0;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const float2 z = col[(rb + r) * LD];
     p[r] = cabs2(z);
-    if (r >= 1 && r <= 8) {
+    if constexpr ((CP & 16) != 0) {
+      // 16-B stores: lane pairs swap one value per row pair (DPP quad_perm [1,0,3,2]), then the even lane stores
+      // row r - 2 at columns (j, j + 1) and the odd lane row r - 1 at (j - 1, j)
+      if (r == 1 || r == 3 || r == 5 || r == 7) zp = z;
+      if (r == 2 || r == 4 || r == 6 || r == 8) {
+        const float2 snd = odd ? zp : z;
+        float2 rcv;
+        rcv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd.x), 0xB1, 0xF, 0xF, true));
+        rcv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd.y), 0xB1, 0xF, 0xF, true));
+        const float4 v = odd ? make_float4(rcv.x, rcv.y, z.x, z.y) : make_float4(zp.x, zp.y, rcv.x, rcv.y);
+        float2* q = dst + (size_t)(r - 2 + (odd ? 1 : 0)) * C - (odd ? 1 : 0);
+        st16<(CP & 2) != 0>(reinterpret_cast<float4*>(q), v);
+      }
+    } else if (r >= 1 && r <= 8) {
       if constexpr ((CP & 2) != 0)
         st8<true>(dst + (size_t)(r - 1) * C, z);
       else
@@ -755,6 +770,7 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
       if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 0, 4>;
       if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 0, 7>;
       if (v == 10) kern = k_doppler_detect<C, KB, NT, true, 0, 10>;
+      if (v == 26) kern = k_doppler_detect<C, KB, NT, true, 0, 26>;
     }
   }
   if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {
