@@ -1,0 +1,54 @@
+"""K1 tile scheduling: the per-XCD dequeue (default, rsl_fft.hip `k_range_fft_p<..., DYN = true>`) against the static
+persistent walk (RSL_RF_DYN=0), on the same device cubes. Scheduling must not change a single bit of the range
+spectra, RDS, peak masks or peak powers: grids below 8 workgroups (static fallback), tile counts that do not divide
+over the 8 XCDs, and batches far larger than the resident grid; then 20 more launches on the default path, so every
+queue slot (8, round-robin) has been reused after its self-reset.
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {  # name: (F, A, C, T_c)  -> K1 tiles = F * A * ceil(C / 8) at S = 512
+    'below8': (1, 1, 16, 51.2e-6),       # 2 tiles: grid < 8, static walk
+    'ragged': (3, 3, 24, 51.2e-6),       # 27 tiles over 8 XCDs (3 or 4 each)
+    'cfg1': (5, 8, 64, 25.6e-6),         # S = 256
+    'cfg2': (40, 8, 128, 51.2e-6),       # 5120 tiles: 6.7 per resident workgroup
+}
+
+
+def _run(ctx, ch, cube, dyn):
+    old = os.environ.get('RSL_RF_DYN')
+    os.environ['RSL_RF_DYN'] = dyn
+    try:
+        ch.work.zero_()
+        ch.rds.zero_()
+        ch.peak_pow.zero_()
+        ctx.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                       row_count=ch.row_count, peak_pow=ch.peak_pow, dc_removal=True)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop('RSL_RF_DYN', None)
+        else:
+            os.environ['RSL_RF_DYN'] = old
+    return [t.clone() for t in (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow)]
+
+
+@pytest.mark.parametrize('name', list(SHAPES))
+def test_dequeue_matches_static_walk(ctx, name):
+    import rsl
+    F, A, C, Tc = SHAPES[name]
+    ch = rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, ctx)
+    S = ch.rds.shape[2]
+    g = torch.Generator(device='cuda').manual_seed(7)
+    cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
+                         torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
+    ref = _run(ctx, ch, cube, '0')
+    assert ref[1].abs().amax().item() > 0
+    for rep in range(21):
+        got = _run(ctx, ch, cube, '1')
+        for a, b, what in zip(ref, got, ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
+            assert torch.equal(a, b), f'{name}: {what} differs on launch {rep}'
