@@ -181,6 +181,9 @@ def main():
         evB = [torch.cuda.Event() for _ in range(2)]
         used = [False, False]
 
+    # 0: offsets + compaction on the front stream; 1: compaction on the back stream; 2: both on the back stream
+    EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '1'))
+
     def step_pipelined(i):
         k = i % 2
         ch = chains[k]
@@ -188,11 +191,11 @@ def main():
         with torch.cuda.stream(sA):
             if used[k]:
                 sA.wait_event(evB[k])  # batch i-2's back half is done with these buffers
-            ch.run_front(cubes[i % nb])
+            ch.run_front(cubes[i % nb], emit=EMIT_BACK == 0, offsets=EMIT_BACK < 2)
             evA[k].record(sA)
         with torch.cuda.stream(sB):
             sB.wait_event(evA[k])
-            ch.run_back()
+            ch.run_back(emit=EMIT_BACK > 0, offsets=EMIT_BACK == 2)
             reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
             evB[k].record(sB)
         used[k] = True

@@ -105,8 +105,9 @@ class RadarChain:
         self.run_front(cube)
         self.run_back(esprit=esprit, velocity=velocity)
 
-    def run_front(self, cube):
-        """Memory-bound half: RDS + detection, offsets, peak / cell compaction (current stream)."""
+    def run_front(self, cube, *, emit: bool = True, offsets: bool = True):
+        """Memory-bound half: RDS + detection, offsets, peak / cell compaction (current stream). With emit=False the
+        compaction is left to run_back(emit=True) (a pipelining split of the same work)."""
         ctx, cfg = self.ctx, self.cfg
         if self.F == 0:  # empty batch: only the (zeroed) bases
             ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
@@ -114,16 +115,27 @@ class RadarChain:
         group = ctx.rds_detect(cube, self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds, work=self.work,
                                mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow,
                                dc_removal=cfg.dc_removal)
-        ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
-        ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists,
-                 peak_pow=self.peak_pow, peak_pow_group=group)
+        self._group = group
+        if offsets:
+            ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
+        if emit:
+            self._emit()
 
-    def run_back(self, *, esprit: bool = True, velocity: bool = True):
-        """Compute-bound half: DoA scan (+ ESPRIT, phase) and the velocity solve, on run_front's lists."""
+    def _emit(self):
+        self.ctx.emit(self.rds, self.mask, self.offs, self.entry_cap, self.cell_cap, want_pdb=True, bufs=self.lists,
+                      peak_pow=self.peak_pow, peak_pow_group=self._group)
+
+    def run_back(self, *, esprit: bool = True, velocity: bool = True, emit: bool = False, offsets: bool = False):
+        """Compute-bound half: DoA scan (+ ESPRIT, phase) and the velocity solve, on run_front's lists (emit=True:
+        the compaction first, after run_front(emit=False))."""
         ctx, cfg = self.ctx, self.cfg
         L = self.lists
         if self.F == 0:
             return
+        if offsets:
+            ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
+        if emit:
+            self._emit()
         if self.fused_doa:
             ctx.doa_extras(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
                            n_dev=self.ncell_dev, esprit_scale=self.esprit_scale, out_idx=self.gidx,
