@@ -95,7 +95,7 @@ def test_process_targets_vs_golden(data, name):
     st = O.steering_matrix(O.azimuth_grid(), int(z['A']))
     idx = np.array([np.argmin(np.abs(est.azimuth_grid - t['azimuth_deg'])) for t in tm])
     nm, nu, _ = P.doa_diff(idx, z['sig'], st, 'music')
-    assert nu == 0 and nm <= max(1, 2e-3 * len(sel))
+    assert nu == 0 and nm <= P.doa_flip_budget(len(sel)), (nm, nu)
     assert np.abs(np.array([t['spatial_signature'] for t in tm]) - z['sig']).max() < 1e-5
     spec = np.array([t['spectrum'] for t in tm[:len(z['music_spec'])]])
     rs = z['music_spec']
@@ -107,7 +107,7 @@ def test_process_targets_vs_golden(data, name):
     tb = est.process_targets(ref, {'peaks': peaks}, 'beamforming')
     idx = np.array([np.argmin(np.abs(est.azimuth_grid - t['azimuth_deg'])) for t in tb])
     nm, nu, _ = P.doa_diff(idx, z['sig'], st, 'beamforming')
-    assert nu == 0
+    assert nu == 0 and nm <= P.doa_flip_budget(len(sel)), (nm, nu)
     bs = np.array([t['spectrum'] for t in tb[:len(z['bf_spec'])]])
     assert np.abs(bs - z['bf_spec']).max() < 1e-4
     assert est.process_targets(ref, {'peaks': peaks[:3]}, 'capon') == []

@@ -69,7 +69,7 @@ def test_step3_extract_angles(staged):
         grid = O.azimuth_grid()
         idx = np.array([int(np.argmin(np.abs(grid - t['azimuth_deg']))) for t in targets])
         nm, nu, _ = P.doa_diff(idx, sigs, O.steering_matrix(grid, A), 'music')
-        assert nu == 0 and nm <= max(1, 2e-3 * len(targets))
+        assert nu == 0 and nm <= P.doa_flip_budget(len(targets)), (nm, nu)
 
 
 def test_step4_velocity_quirk(staged):
