@@ -1,10 +1,14 @@
-"""Velocity-to-pose integration (host, NumPy/SciPy) for the drop-in import path.
+"""Velocity-to-pose integration for the drop-in import path, on the device.
 
 Drop-in for ``src/pose_integration/pose_integration.py`` of the reference (``PoseIntegrator`` :23-378,
-``integrate_velocities_to_pose`` :381-424).  This is the post-gather trajectory reduction (SURVEY §8f
-"next" #1): it runs on the host over the gathered per-frame velocities (6 floats per frame).  The
-reference's ``integrate_pose`` multiplies norm(omega)[N] by diff(t)[N-1] (:199) and therefore raises
-ValueError for N >= 2; that observable behaviour is kept.
+``integrate_velocities_to_pose`` :381-424).  ``integrate_translational_velocity`` and
+``integrate_angular_velocity`` run the fp64 prefix scans of librsl (``rsl_traj_scan``: trapezoid / Euler
+positions and the quaternion product of the rotation-vector increments, with the reference's per-step
+``np.diff(timestamps)``) and the ``uniform_filter1d(mode='nearest')`` smoothing (``rsl_traj_smooth``); the host
+only converts the device quaternions to the reference's rotation matrices and 'xyz' Euler angles.  Like every
+class of this package, it needs the HIP device (no CPU fallback).  The reference's ``integrate_pose`` multiplies
+norm(omega)[N] by diff(t)[N-1] (:199) and therefore raises ValueError for N >= 2; that observable behaviour is
+kept.
 """
 from __future__ import annotations
 
@@ -15,6 +19,25 @@ import numpy as np
 from scipy.spatial.transform import Rotation
 
 logger = logging.getLogger(__name__)
+
+_METHODS = {'trapezoidal': 0, 'euler': 1}
+
+
+def _scan(vel, nv, omega, timestamps, method):
+    """Device scan of one frame sequence -> (ctx, pos [N, 3], quat [N, 4]) device tensors, pose 0 = origin / identity."""
+    import torch
+    import rsl
+    from rsl.runtime import _ptr
+    ctx = rsl.get_context()
+    ts = np.ascontiguousarray(timestamps, dtype=np.float64)
+    N = len(ts)
+    dv = ctx.to_dev(np.ascontiguousarray(vel, dtype=np.float64).reshape(N, -1))
+    dw = ctx.to_dev(np.ascontiguousarray(omega, dtype=np.float64).reshape(N, 3)) if omega is not None else None
+    pos, quat = ctx.empty((N, 3), torch.float64), ctx.empty((N, 4), torch.float64)
+    ctx._bind()
+    ctx.check(ctx.lib.rsl_traj_scan(ctx.h, _ptr(dv), int(dv.shape[1]), int(nv), _ptr(dw), 3, _ptr(ctx.to_dev(ts)),
+                                    0.0, N, method, _ptr(pos), _ptr(quat), None), 'rsl_traj_scan')
+    return ctx, pos, quat
 
 
 class PoseIntegrator:
@@ -32,46 +55,41 @@ class PoseIntegrator:
         self.current_rotation = Rotation.from_euler('xyz', self.initial_orientation)
 
     def integrate_translational_velocity(self, velocities: np.ndarray, timestamps: np.ndarray) -> np.ndarray:
-        """Trapezoid / Euler running sum (:67-111), then uniform_filter1d(mode='nearest') smoothing."""
+        """Trapezoid / Euler running sum (:67-103) as a device prefix scan, then the :105-109 smoothing."""
+        if self.integration_method not in _METHODS:
+            raise ValueError(f"Unknown integration method: {self.integration_method}")
         v = np.asarray(velocities, dtype=np.float64)
         N = len(v)
-        dt = np.diff(timestamps)
-        if self.integration_method == 'trapezoidal':
-            inc = 0.5 * dt[:, None] * (v[:-1] + v[1:])
-        elif self.integration_method == 'euler':
-            inc = dt[:, None] * v[:-1]
-        else:
-            raise ValueError(f"Unknown integration method: {self.integration_method}")
-        pos = np.zeros((N, 3))
-        pos[0] = self.initial_position
-        for i in range(1, N):  # sequential sum, same rounding order as the reference loop
-            pos[i] = pos[i - 1] + inc[i - 1]
+        if N == 0:
+            np.zeros((0, 3))[0] = self.initial_position  # the reference's positions[0] = ... on an empty array
+        ctx, pos, _ = _scan(v.reshape(N, -1)[:, :3], min(3, v.reshape(N, -1).shape[1]), None, timestamps,
+                            _METHODS[self.integration_method])
+        pos += ctx.torch.as_tensor(self.initial_position, dtype=ctx.torch.float64, device=pos.device)
         if self.smoothing and N > self.smoothing_window:
-            from scipy.ndimage import uniform_filter1d
-            for c in range(3):
-                pos[:, c] = uniform_filter1d(pos[:, c], size=self.smoothing_window, mode='nearest')
-        return pos
+            from rsl.traj import smooth
+            pos = smooth(ctx, pos, int(self.smoothing_window))
+        return pos.cpu().numpy()
 
     def integrate_angular_velocity(self, angular_velocities: np.ndarray,
                                    timestamps: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-        """Right-multiplied rotation-vector increments (:113-167)."""
-        w = np.asarray(angular_velocities, dtype=np.float64)
+        """Right-multiplied rotation-vector increments (:113-167) as a device quaternion prefix product; a step
+        with |omega| <= 1e-12 copies the previous orientation and rotation (:162-165)."""
+        w = np.asarray(angular_velocities, dtype=np.float64).reshape(-1, 3)
         N = len(w)
         ori = np.zeros((N, 3))
         ori[0] = self.initial_orientation
         rot = np.zeros((N, 3, 3))
         rot[0] = self.current_rotation.as_matrix()
-        dt = np.diff(timestamps)
-        for i in range(1, N):
-            om = w[i - 1]
-            mag = np.linalg.norm(om)
-            if mag > 1e-12:
-                r = Rotation.from_matrix(rot[i - 1]) * Rotation.from_rotvec((om / mag) * (mag * dt[i - 1]))
-                rot[i] = r.as_matrix()
-                ori[i] = r.as_euler('xyz')
-            else:
-                rot[i] = rot[i - 1]
-                ori[i] = ori[i - 1]
+        if N < 2:
+            return ori, rot
+        _, _, quat = _scan(w, 0, w, timestamps, 0)
+        q = quat.cpu().numpy()
+        r = self.current_rotation * Rotation.from_quat(q[1:, [1, 2, 3, 0]])
+        moved = np.linalg.norm(w[:-1], axis=1) > 1e-12
+        src = np.maximum.accumulate(np.where(np.concatenate([[True], moved]), np.arange(N), 0))
+        rot[1:] = r.as_matrix()
+        ori[1:] = r.as_euler('xyz')
+        rot, ori = rot[src], ori[src]  # unmoved steps repeat the last moved one (or the initial pose) exactly
         return ori, rot
 
     def integrate_pose(self, velocities: np.ndarray, angular_velocities: np.ndarray, timestamps: np.ndarray) -> Dict:

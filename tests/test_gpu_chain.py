@@ -22,7 +22,9 @@ CFGS = {  # name: (A, C, T_c)
     'cfg5': (16, 256, 102.4e-6),  # configs[4] frame shape (A16 C256 S1024), one frame
     'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
     'a4': (4, 64, 25.6e-6),  # fewer antennas than the DoA kernel's width (zero-padded signature, per-element ESPRIT)
+    'cfg1_ridge': (8, 64, 25.6e-6),  # regularised LS velocity (ridge 0.01 on v, velocity_solver_improved.py:261)
 }
+RIDGE = {'cfg1_ridge': 0.01}
 FRAMES = {'cfg5': 1}
 DOA_SAMPLE = 30000  # cells checked per frame against the oracle scan (random subset above this; cfg5 has ~207 K)
 
@@ -42,7 +44,7 @@ def runs(ctx):
     for name, (A, C, Tc) in CFGS.items():
         F = FRAMES.get(name, 2)
         frames = make_frames(A, C, Tc, F, 1000)
-        cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
+        cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=RIDGE.get(name, 0.0))
         ch = rsl.RadarChain(cfg, F, ctx)
         cube = ctx.to_dev(frames.astype(np.complex64))
         if name.endswith('_onepass'):
@@ -141,7 +143,7 @@ def test_velocity_parity(runs, name):
         w = np.array([bin(int(m) & 0xffffffff).count('1') for m in r['c_amask'][sl]])
         az = np.repeat(np.radians(grid[r['gidx'][sl]]), w)
         y = np.repeat(r['phase'][sl], w)
-        vx, vy, cost = O.velocity_ls(az, y, lambda_c=3e8 / cfg.fc)
+        vx, vy, cost = O.velocity_ls(az, y, lambda_c=3e8 / cfg.fc, ridge=cfg.ridge)
         v = r['velocity'][f]
         assert abs(v[2] - cost) <= P.VEL_COST_RTOL * cost
         assert abs(v[0] - vx) < P.VEL_ATOL and abs(v[1] - vy) < P.VEL_ATOL
@@ -177,14 +179,14 @@ def test_velocity_end_to_end(runs, name):
         sigs = np.stack([O.spatial_signature(ref, ii, jj) for ii, jj in zip(i, j)])
         ridx = _oracle_argmax(sigs, steer)
         ph = O.observed_phase(sigs)
-        vx, vy, cost = O.velocity_ls(np.radians(grid[ridx]), ph, lambda_c=lam)
+        vx, vy, cost = O.velocity_ls(np.radians(grid[ridx]), ph, lambda_c=lam, ridge=cfg.ridge)
         v = r['velocity'][f]
         same_set = len(ga) == len(a) and (ga == a).all() and (gi == i).all() and (gj == j).all()
         # the GPU's grid index per entry, through its cell list
         cell_of = {int(rc): k for k, rc in enumerate(r['c_rc'][cb[f]:cb[f + 1]])}
         gidx_e = np.array([r['gidx'][cb[f] + cell_of[int(ii) * C + int(jj)]] if int(ii) * C + int(jj) in cell_of
                            else ridx[n] for n, (ii, jj) in enumerate(zip(i, j))])
-        mx, my, mcost = O.velocity_ls(np.radians(grid[gidx_e]), ph, lambda_c=lam)
+        mx, my, mcost = O.velocity_ls(np.radians(grid[gidx_e]), ph, lambda_c=lam, ridge=cfg.ridge)
         nflip = int((gidx_e != ridx).sum())
         scale = max(abs(mx), abs(my), 1e-12)
         print(f'{name} frame {f}: v_ref ({vx:.6e}, {vy:.6e}) v_gpu ({v[0]:.6e}, {v[1]:.6e}) '
