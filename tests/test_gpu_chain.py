@@ -20,7 +20,7 @@ CFGS = {  # name: (A, C, T_c)
     'cfg2': (8, 128, 51.2e-6),
     'cfg5a16': (16, 32, 12.8e-6),
     'cfg5': (16, 256, 102.4e-6),  # configs[4] frame shape (A16 C256 S1024), one frame
-    'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
+    'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass range-class RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
     'a4': (4, 64, 25.6e-6),  # fewer antennas than the DoA kernel's width (zero-padded signature, per-element ESPRIT)
     'cfg1_ridge': (8, 64, 25.6e-6),  # regularised LS velocity (ridge 0.01 on v, velocity_solver_improved.py:261)
 }
