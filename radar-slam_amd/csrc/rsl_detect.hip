@@ -66,43 +66,62 @@ __global__ __launch_bounds__(256) void k_detect(const float2* __restrict__ rds, 
   }
 }
 
-// Exclusive scan of n ints (global) into out (global) by one 1024-thread block; returns total.
+// Exclusive scan of one value per thread over an NT-thread block (wave shuffles + one LDS round); *total = the sum.
+template <int NT>
+__device__ long long block_exscan(long long v, long long* lds, long long* total) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  long long inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long u = __shfl_up(inc, d);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) lds[w] = inc;
+  __syncthreads();
+  long long base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) {
+    const long long x = lds[k];
+    base += k < w ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+// Exclusive scan of n ints (global) into out (global) by one NT-thread block; returns total.
+template <int NT>
 __device__ long long block_scan_global(const int* in, int* out, int n, long long* lds) {
   const int t = threadIdx.x;
-  const int per = (n + 1023) / 1024;
+  const int per = (n + NT - 1) / NT;
   const int b = t * per, e = min(n, b + per);
   long long s = 0;
   for (int k = b; k < e; ++k) s += in[k];
-  lds[t] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const long long v = (t >= off) ? lds[t - off] : 0;
-    __syncthreads();
-    lds[t] += v;
-    __syncthreads();
-  }
-  long long run = lds[t] - s;
-  const long long total = lds[1023];
+  long long total;
+  long long run = block_exscan<NT>(s, lds, &total);
   for (int k = b; k < e; ++k) {
     const int v = in[k];
     out[k] = (int)run;
     run += v;
   }
-  __syncthreads();
   return total;
 }
 
-// One block per frame: entry offsets over (antenna, range) rows and union-cell offsets over range rows.
-__global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __restrict__ mask,
-                                                  const int* __restrict__ row_count, int A, int S, int W,
-                                                  int* __restrict__ entry_row_off, int* __restrict__ cell_row_off,
-                                                  int* __restrict__ cell_row_cnt, long long* __restrict__ frame_counts,
-                                                  unsigned long long* __restrict__ umask) {
-  __shared__ long long lds[1024];
+// One block per frame: entry offsets over (antenna, range) rows and union-cell offsets over range rows.  NT = 256:
+// small blocks get CU slots between the long-lived DoA blocks of the other batch in the pipelined chain (a 1024-thread
+// block waits for a whole CU to drain).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_offsets(const unsigned long long* __restrict__ mask,
+                                                const int* __restrict__ row_count, int A, int S, int W,
+                                                int* __restrict__ entry_row_off, int* __restrict__ cell_row_off,
+                                                int* __restrict__ cell_row_cnt, long long* __restrict__ frame_counts,
+                                                unsigned long long* __restrict__ umask) {
+  __shared__ long long lds[NT / 64];
   const long f = blockIdx.x;
-  const long long te = block_scan_global(row_count + f * A * S, entry_row_off + f * A * S, A * S, lds);
+  const long long te = block_scan_global<NT>(row_count + f * A * S, entry_row_off + f * A * S, A * S, lds);
   const unsigned long long* mf = mask + (size_t)f * A * S * W;
-  for (int i = threadIdx.x; i < S; i += 1024) {
+  for (int i = threadIdx.x; i < S; i += NT) {
     int c = 0;
     for (int w = 0; w < W; ++w) {
       unsigned long long u = 0;
@@ -113,7 +132,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __re
     cell_row_cnt[f * S + i] = c;
   }
   __syncthreads();
-  const long long tc = block_scan_global(cell_row_cnt + f * S, cell_row_off + f * S, S, lds);
+  const long long tc = block_scan_global<NT>(cell_row_cnt + f * S, cell_row_off + f * S, S, lds);
   if (threadIdx.x == 0) {
     frame_counts[2 * f] = te;
     frame_counts[2 * f + 1] = tc;
@@ -121,38 +140,31 @@ __global__ __launch_bounds__(1024) void k_offsets(const unsigned long long* __re
 }
 
 // One block: exclusive scan over frames -> entry_base[F+1], cell_base[F+1].
-__global__ __launch_bounds__(1024) void k_frame_scan(const long long* __restrict__ frame_counts, int F,
-                                                     long long* __restrict__ entry_base,
-                                                     long long* __restrict__ cell_base) {
-  __shared__ long long le[1024], lc[1024];
+template <int NT>
+__global__ __launch_bounds__(NT) void k_frame_scan(const long long* __restrict__ frame_counts, int F,
+                                                   long long* __restrict__ entry_base,
+                                                   long long* __restrict__ cell_base) {
+  __shared__ long long lds[NT / 64];
   const int t = threadIdx.x;
-  const int per = (F + 1023) / 1024;
+  const int per = (F + NT - 1) / NT;
   const int b = t * per, e = min(F, b + per);
   long long se = 0, sc = 0;
   for (int k = b; k < e; ++k) {
     se += frame_counts[2 * k];
     sc += frame_counts[2 * k + 1];
   }
-  le[t] = se;
-  lc[t] = sc;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const long long ve = (t >= off) ? le[t - off] : 0, vc = (t >= off) ? lc[t - off] : 0;
-    __syncthreads();
-    le[t] += ve;
-    lc[t] += vc;
-    __syncthreads();
-  }
-  long long re = le[t] - se, rc = lc[t] - sc;
+  long long tot_e, tot_c;
+  long long re = block_exscan<NT>(se, lds, &tot_e);
+  long long rc = block_exscan<NT>(sc, lds, &tot_c);
   for (int k = b; k < e; ++k) {
     entry_base[k] = re;
     cell_base[k] = rc;
     re += frame_counts[2 * k];
     rc += frame_counts[2 * k + 1];
   }
-  if (t == 1023) {
-    entry_base[F] = le[1023];
-    cell_base[F] = lc[1023];
+  if (t == 0) {
+    entry_base[F] = tot_e;
+    cell_base[F] = tot_c;
   }
 }
 
@@ -541,11 +553,20 @@ hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const 
                           long long* cell_base, long long* frame_counts, unsigned long long* umask) {
   if (F <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
-  hipLaunchKernelGGL(k_offsets, dim3(F), dim3(1024), 0, st, mask, row_count, A, S, W, entry_row_off, cell_row_off,
-                     cell_row_cnt, frame_counts, umask);
+  static const int nt = [] {
+    const char* e = getenv("RSL_OFF_NT");
+    return e ? atoi(e) : 256;
+  }();
+  if (nt == 1024) {
+    hipLaunchKernelGGL(k_offsets<1024>, dim3(F), dim3(1024), 0, st, mask, row_count, A, S, W, entry_row_off,
+                       cell_row_off, cell_row_cnt, frame_counts, umask);
+  } else {
+    hipLaunchKernelGGL(k_offsets<256>, dim3(F), dim3(256), 0, st, mask, row_count, A, S, W, entry_row_off,
+                       cell_row_off, cell_row_cnt, frame_counts, umask);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_frame_scan, dim3(1), dim3(1024), 0, st, frame_counts, F, entry_base, cell_base);
+  hipLaunchKernelGGL(k_frame_scan<256>, dim3(1), dim3(256), 0, st, frame_counts, F, entry_base, cell_base);
   return hipGetLastError();
 }
 
