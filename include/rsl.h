@@ -229,6 +229,23 @@ int rsl_traj_stitch(rsl_handle h, const void* summaries, int R, int rank, double
 /* uniform_filter1d(x[:, c], size, mode='nearest') per column (pose_integration.py:105-109); x, out f64 [F][ncol]. */
 int rsl_traj_smooth(rsl_handle h, const void* x, long long F, int ncol, int size, void* out);
 
+/* SURVEY §8f #3 (evaluation half)  PoseErrorEvaluator (evaluation/compute_pose_error.py:51-361), fp64.
+ *     Poses f64 [n][7] = (x, y, z, q0, q1, q2, q3) with q read as scipy quaternions (scalar LAST, normalised), as the
+ *     reference's Rotation.from_quat reads them.  scratch >= rsl_pose_error_scratch_bytes(n, nlen) (device).
+ *     rsl_pose_align (align_trajectories :51-96 + compute_ape :171-236): align f64 [32] = position rotation R (9,
+ *       row-major; Umeyama :98-140), translation t (3), orientation rotation Rq (9; Rotation.mean of gt * est^-1,
+ *       :142-169), its quaternion (4, x y z w, w >= 0), scale_factor = cbrt(det R) (1), the two position means (6);
+ *       aligned f64 [n][7]; ape_err f64 [3][n] = position, orientation, combined errors; ape_stats f64 [3][5]
+ *       (nullable) = {rmse, mean, std, max, n} per series.
+ *     rsl_pose_rte (compute_rte :238-306 on rsl_pose_align's aligned poses): lengths f64 [nlen] (device) segment
+ *       lengths; err f64 [nlen][n]: the first counts[l] entries of row l are the segment errors (the valid starts of a
+ *       positive length are a prefix); counts u64 [nlen]; stats f64 [nlen][5] as above. */
+long long rsl_pose_error_scratch_bytes(long long n, int nlen);
+int rsl_pose_align(rsl_handle h, const void* est, const void* gt, long long n, void* scratch, void* align,
+                   void* aligned, void* ape_err, void* ape_stats);
+int rsl_pose_rte(rsl_handle h, const void* aligned, const void* gt, long long n, const void* lengths, int nlen,
+                 void* scratch, void* err, void* counts, void* stats);
+
 /* SURVEY §8f #2  FMCWRadarSimulator.synthesize_frame (scripts/simulate_raw.py:147-221) at batch scale.
  *     rsl_synth_pattern: the deterministic part, which does not depend on the chirp index, as fp64 complex
  *       pattern [A][S] (device) from scatterers f64 [n][4] = {range m, azimuth rad, rcs dBsm, radial velocity m/s}

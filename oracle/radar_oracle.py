@@ -554,3 +554,90 @@ def integrate_rotations(om, ts, r0=None):
         else:
             rot[i] = rot[i - 1]
     return rot
+
+
+# ----------------------------------------------------------------------------------------
+# L5: pose error evaluation (evaluation/compute_pose_error.py) — SURVEY §8f #3, evaluation half
+# ----------------------------------------------------------------------------------------
+def umeyama(source, target):
+    """compute_pose_error.py:98-140: centred cross-covariance H = S_c^T T_c, svd, R = V U^T with the
+    det < 0 flip of the last row of Vt, t = mean(T) - R mean(S).  Returns (aligned source, T [4, 4])."""
+    sc = source - np.mean(source, axis=0)
+    tc = target - np.mean(target, axis=0)
+    U, _, Vt = np.linalg.svd(sc.T @ tc)
+    R = Vt.T @ U.T
+    if np.linalg.det(R) < 0:
+        Vt[-1, :] *= -1
+        R = Vt.T @ U.T
+    t = np.mean(target, axis=0) - R @ np.mean(source, axis=0)
+    T = np.eye(4)
+    T[:3, :3], T[:3, 3] = R, t
+    return (R @ source.T).T + t, T
+
+
+def align_orientations(source_quats, target_quats):
+    """compute_pose_error.py:142-169: quaternions in scipy order (scalar last); mean of target * source^-1
+    (Rotation.mean: principal eigenvector of sum q q^T), aligned = source * mean.  Returns (quats, R [3, 3])."""
+    from scipy.spatial.transform import Rotation
+    s, t = Rotation.from_quat(source_quats), Rotation.from_quat(target_quats)
+    avg = (t * s.inv()).mean()
+    return (s * avg).as_quat(), avg.as_matrix()
+
+
+def align_trajectories(est, gt):
+    """compute_pose_error.py:51-96 -> (aligned [N, 7], T [4, 4], info)."""
+    ap, Tp = umeyama(est[:, :3], gt[:, :3])
+    aq, Rq = align_orientations(est[:, 3:7], gt[:, 3:7])
+    T = np.eye(4)
+    T[:3, :3], T[:3, 3] = Rq, Tp[:3, 3]
+    info = {'position_translation': Tp[:3, 3], 'position_rotation': Tp[:3, :3], 'orientation_rotation': Rq,
+            'scale_factor': np.linalg.det(Tp[:3, :3]) ** (1 / 3)}
+    return np.column_stack([ap, aq]), T, info
+
+
+def _stats(x, pre):
+    return {f'{pre}_rmse': np.sqrt(np.mean(x ** 2)), f'{pre}_mean': np.mean(x), f'{pre}_std': np.std(x),
+            f'{pre}_max': np.max(x)}
+
+
+def ape(est, gt):
+    """compute_pose_error.py:171-236 (vectorised over poses)."""
+    from scipy.spatial.transform import Rotation
+    aligned, _, info = align_trajectories(est, gt)
+    pe = np.linalg.norm(aligned[:, :3] - gt[:, :3], axis=1)
+    oe = np.linalg.norm((Rotation.from_quat(gt[:, 3:7]) * Rotation.from_quat(aligned[:, 3:7]).inv()).as_rotvec(),
+                        axis=1)
+    ce = np.sqrt(pe ** 2 + oe ** 2)
+    out = {'position_errors': pe, 'orientation_errors': oe, 'pose_errors': ce}
+    for x, pre in ((pe, 'position'), (oe, 'orientation'), (ce, 'pose')):
+        out.update(_stats(x, pre))
+    out['alignment_info'] = info
+    return out
+
+
+def rte(est, gt, lengths=(100, 200, 300, 400, 500, 600, 700, 800)):
+    """compute_pose_error.py:238-361 (vectorised over start poses): segment end = searchsorted of the aligned
+    estimate's travelled distance (:308-322); error = |inv(T_est) T_gt| as (translation norm, Frobenius norm of
+    R - I) (:324-361); a length with no segment has no entry."""
+    from scipy.spatial.transform import Rotation
+    aligned, _, _ = align_trajectories(est, gt)
+    ep, gp = aligned[:, :3], gt[:, :3]
+    d = np.concatenate([[0], np.cumsum(np.linalg.norm(np.diff(ep, axis=0), axis=1))])
+    Re, Rg = Rotation.from_quat(aligned[:, 3:7]).as_matrix(), Rotation.from_quat(gt[:, 3:7]).as_matrix()
+    out = {}
+    N = len(ep)
+    for L in lengths:
+        i = np.arange(N)
+        end = np.searchsorted(d, d + L)
+        ok = (end < N) & (end > i)
+        i, end = i[ok], end[ok]
+        if len(i) == 0:
+            continue
+        R1 = np.einsum('nij,nkj->nik', Re[end], Re[i])   # rot2 * rot1.inv()
+        R2 = np.einsum('nij,nkj->nik', Rg[end], Rg[i])
+        te = np.linalg.norm(np.einsum('nji,nj->ni', R1, (gp[end] - gp[i]) - (ep[end] - ep[i])), axis=1)
+        re = np.linalg.norm(np.einsum('nji,njk->nik', R1, R2) - np.eye(3), axis=(1, 2))
+        err = np.sqrt(te ** 2 + re ** 2)
+        out[f'rte_{L:.0f}m'] = {'errors': err, 'rmse': np.sqrt(np.mean(err ** 2)), 'mean': np.mean(err),
+                                 'std': np.std(err), 'max': np.max(err), 'num_segments': len(err)}
+    return out

@@ -634,3 +634,36 @@ int rsl_synth_cube(rsl_handle h, const void* pattern, int F, int A, int C, int S
                                           (float2*)cube),
                    "synth_cube");
 }
+
+long long rsl_pose_error_scratch_bytes(long long n, int nlen) {
+  if (n < 0 || nlen < 0) return -1;
+  return 8 * rsl::pose_error_scratch_doubles(n, nlen);
+}
+
+int rsl_pose_align(rsl_handle h, const void* est, const void* gt, long long n, void* scratch, void* align,
+                   void* aligned, void* ape_err, void* ape_stats) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 1) return fail(h, RSL_ERR_INVALID, "rsl_pose_align: need at least one pose");
+  if (!est || !gt || !scratch || !align || !aligned || !ape_err)
+    return fail(h, RSL_ERR_INVALID, "rsl_pose_align: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_pose_align(h->stream, (const double*)est, (const double*)gt, n, (double*)scratch,
+                                          (double*)align, (double*)aligned, (double*)ape_err, (double*)ape_stats),
+                   "pose_align");
+}
+
+int rsl_pose_rte(rsl_handle h, const void* aligned, const void* gt, long long n, const void* lengths, int nlen,
+                 void* scratch, void* err, void* counts, void* stats) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 1 || nlen < 0 || nlen > 1024) return fail(h, RSL_ERR_INVALID, "rsl_pose_rte: bad arguments");
+  if (nlen == 0) return RSL_OK;
+  if (!aligned || !gt || !lengths || !scratch || !err || !counts || !stats)
+    return fail(h, RSL_ERR_INVALID, "rsl_pose_rte: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_pose_rte(h->stream, (const double*)aligned, (const double*)gt, n,
+                                        (const double*)lengths, nlen, (double*)scratch, (double*)err,
+                                        (unsigned long long*)counts, (double*)stats),
+                   "pose_rte");
+}

@@ -102,6 +102,12 @@ hipError_t launch_traj_apply(hipStream_t st, double* pos, double* quat, long F, 
 hipError_t launch_traj_stitch(hipStream_t st, const double* summ, int R, int rank, double dt, int method,
                               double* state, double* base);
 hipError_t launch_traj_smooth(hipStream_t st, const double* x, long F, int ncol, int size, double* out);
+// Pose-error evaluation (rsl_eval.hip): Umeyama + quaternion-mean alignment, APE errors / statistics, RTE.
+long long pose_error_scratch_doubles(long long n, int nlen);
+hipError_t launch_pose_align(hipStream_t st, const double* est, const double* gt, long n, double* scratch,
+                             double* align, double* aligned, double* ape_err, double* ape_stats);
+hipError_t launch_pose_rte(hipStream_t st, const double* aligned, const double* gt, long n, const double* len,
+                           int nlen, double* scratch, double* err, unsigned long long* cnt, double* stats);
 
 }  // namespace rsl
 

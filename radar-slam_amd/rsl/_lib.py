@@ -64,6 +64,9 @@ SIGNATURES = {
     'rsl_traj_smooth': (c_int, [_P, _P, c_longlong, c_int, c_int, _P]),
     'rsl_synth_pattern': (c_int, [_P, _P, c_int, c_int, c_int, c_double, c_double, c_double, c_double, _P]),
     'rsl_synth_cube': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_ulonglong, c_longlong, _P]),
+    'rsl_pose_error_scratch_bytes': (c_longlong, [c_longlong, c_int]),
+    'rsl_pose_align': (c_int, [_P, _P, _P, c_longlong, _P, _P, _P, _P, _P]),
+    'rsl_pose_rte': (c_int, [_P, _P, _P, c_longlong, _P, c_int, _P, _P, _P, _P]),
     'rsl_bvls': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, _P, _P, _P]),
 }
 

@@ -16,6 +16,7 @@ MODULES = {
     'src.pose_integration.pose_integration': 'src/pose_integration/pose_integration.py',
     'src.algorithms.velocity_solver_improved': 'src/algorithms/velocity_solver_improved.py',
     'src.algorithms.advanced_velocity_optimization': 'src/algorithms/advanced_velocity_optimization.py',
+    'evaluation.compute_pose_error': 'evaluation/compute_pose_error.py',
 }
 
 
