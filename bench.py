@@ -156,6 +156,73 @@ def cpu_baseline(procs=16, frames=2, ridge=0.01):
                                       f"MUSIC / ESPRIT over all peaks, LS velocity); {t_vec:.1f} s wall"})
 
 
+def run_spectrum(args, world, rank, local, dev):
+    """configs[1]: 8ch x 128chirp x 512 cube, 1000 frames per step, range-Doppler FFT + peaks + the MUSIC spectrum
+    of every unique cell (f32, grid-major [361, cells]; the reference keeps spectrum f64[G] per target,
+    angle_estimation.py:299).  One chain, no pipelining; the spectrum store dominates (51 MB per frame)."""
+    import torch
+    import torch.distributed as dist
+    import rsl
+    A, C, S, Tc = 8, 128, 512, 51.2e-6
+    F = args.frames_per_step or 1000
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, spectrum=True, cell_frac=0.6)
+    ctx = rsl.get_context(local)
+    ch = rsl.RadarChain(cfg, F, ctx)
+    cubes = make_cubes(ctx, 2, F, A, C, Tc, rank)
+
+    def step(i):
+        ch.run(cubes[i % 2], esprit=False, velocity=False)
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ne, nc = ch.totals()
+    if ne > ch.entry_cap or nc > ch.cell_cap:
+        raise RuntimeError('peak capacity exceeded')
+    if not args.no_timing:
+        ctx.timing(True)
+        ctx.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = ctx.timing_read() if not args.no_timing else {}
+    ctx.timing(False)
+    if rank != 0:
+        return
+    G = len(ch.grid)
+    line = {"metric": "radar frames/sec, range-Doppler FFT + MUSIC spectrum (configs[1]), 8ch x 128chirp x 512",
+            "value": F * args.steps * world / elapsed, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "configs[1]: 8ch x 128chirp x 512 synthetic cube, RDS + peaks + MUSIC spectrum of "
+                                   "every unique cell (f32, cell-blocked [cells/32, 361, 32])", "frames_per_step": F,
+                       "doa_grid": G, "parallelism": f"frame-sharded x{world}"},
+            "peaks_per_frame": ne / F, "cells_per_frame": nc / F}
+    if kt:
+        per = lambda k: kt[k][0] / max(kt[k][1], 1)
+        sbytes = nc * G * 4 + nc * A * 8  # spectrum store + signature gather
+        t = per('doa_scan') * 1e-3
+        line["roofline"] = {"bound": "hbm", "kernel": "k_doa_scan (spectrum)", "achieved": sbytes / t / 1e9,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sbytes / t / 1e9 / HBM_PEAK_GBS,
+                            "traffic": None, "avg_launch_ms": per('doa_scan'), "algorithmic_bytes_per_launch": sbytes}
+        fb = 2 * A * C * S * 8 * F
+        tf = (per('range_fft') + per('doppler_fft')) * 1e-3
+        line["fft_stage"] = {"bound": "hbm", "achieved": fb / tf / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": fb / tf / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fb}
+        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) for k, v in kt.items() if v[1]}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -163,9 +230,11 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--frames-per-step', type=int, default=None,
                     help='frames per GPU per step (default 2000 for cfg2, 100 for cfg5)')
-    ap.add_argument('--config', choices=('cfg2', 'cfg5'), default='cfg2',
+    ap.add_argument('--config', choices=('cfg2', 'cfg5', 'spectrum'), default='cfg2',
                     help='cfg2 = configs[2] (A8 C128 S512, the metric\'s workload); cfg5 = the configs[4] frame shape '
-                         '(A16 C256 S1024), a second measurement, not the metric line')
+                         '(A16 C256 S1024); spectrum = configs[1] (A8 C128 S512, 1000 frames per step: RDS + peaks + '
+                         'the full MUSIC spectrum of every cell, f32 [G, cells]); the last two are second '
+                         'measurements, not the metric line')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-frames', type=int, default=2, help='whole frames of the loop-faithful CPU baseline')
     ap.add_argument('--cpu-procs', type=int, default=16,
@@ -200,6 +269,8 @@ def main():
     torch.cuda.set_device(dev)
 
     import rsl
+    if args.config == 'spectrum':
+        return run_spectrum(args, world, rank, local, dev)
     if args.config == 'cfg5':
         A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 100
     else:

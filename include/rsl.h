@@ -33,6 +33,12 @@ extern "C" {
 #define RSL_METHOD_MUSIC 1
 /* rsl_doa method flag: use the Toeplitz f16-MFMA argmax path (requires RSL_STEER_TOEPLITZ from the table build) */
 #define RSL_DOA_TOEPLITZ 0x100
+/* rsl_doa method flag: out_spec is grid-major f32 [G][ncell] (leading dimension = the list capacity ncell) instead of
+ * cell-major [n][G]; the batched spectrum path (coalesced stores) */
+#define RSL_DOA_SPEC_GMAJOR 0x200
+/* rsl_doa method flag: out_spec is cell-blocked f32 [ceil(ncell / 32)][G][32] (cell c, grid point g at
+ * ((c / 32) G + g) 32 + c % 32): every store is a contiguous run; the batched chain's spectrum layout */
+#define RSL_DOA_SPEC_BLOCKED 0x400
 /* rsl_steer_table_build flags */
 #define RSL_STEER_TOEPLITZ 1
 
@@ -135,8 +141,9 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
  *     steering matrix (needed by MUSIC with RSL_DOA_TOEPLITZ for its exact fp64 near-degenerate re-scan).
  *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; ignored when out_spec is requested).
  *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
- *     at the argmax (unit-norm s); out_spec f32 [n, G] (nullable) = MUSIC 1/(M-|a^H s|^2) with the
- *     reference's den > 1e-12 rule, or the beamforming |a^H s|^2. */
+ *     at the argmax (unit-norm s); out_spec f32 [n, G] (nullable; [G][ncell] with RSL_DOA_SPEC_GMAJOR,
+ *     [ceil(ncell / 32)][G][32] with RSL_DOA_SPEC_BLOCKED) = MUSIC
+ *     1/(M-|a^H s|^2) with the reference's den > 1e-12 rule, or the beamforming |a^H s|^2. */
 int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
             const void* ncell_dev, long long ncell, const void* steer_tab, const void* steer_c128, int G, int method,
             void* out_idx, void* out_gmax, void* out_spec);
@@ -155,6 +162,18 @@ int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const voi
 int rsl_cell_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,
                     const void* ncell_dev, long long ncell, double esprit_scale, const void* gidx,
                     const void* az_table, void* sig_out, void* esprit_deg, void* phase, void* az_out);
+
+/* a13-a15 with num_sources != 1  music_spectrum / estimate_angle_music / estimate_angle_esprit
+ *     (angle_estimation.py:109-225) for any num_sources (Python slicing semantics for K <= 0 and K >= M), fp64:
+ *     sigs c128 [n][M] (device, the signatures as given; MUSIC normalises them), steer_c128 f64 [G][M][2]
+ *     (device), spec f64 [n][G] = 1/den or 0 (den <= 1e-12), deg f64 [n] (0.0 where the reference's ESPRIT
+ *     raises, NaN where it returns NaN).  The reference's noise / null-space bases for 2 <= K < M come from LAPACK
+ *     round-off; these use a fixed Householder completion (rsl_subspace.hip), so only K = 1, K >= M (MUSIC),
+ *     K <= 0 (ESPRIT) and zero signatures are reference-determined. */
+int rsl_music_subspace(rsl_handle h, const void* sigs, long long n, int M, int num_sources, const void* steer_c128,
+                       int G, void* spec);
+int rsl_esprit_subspace(rsl_handle h, const void* sigs, long long n, int M, int num_sources, double esprit_scale,
+                        void* deg);
 
 /* a19  RobustAngleEstimator.compute_angle_confidence (robust_angle_estimation.py:88-138) for n
  *     (cell, grid index) pairs.  steer_c128 f64 [G][M][2] and steer_phase f64 [G][M] = np.angle(a) are

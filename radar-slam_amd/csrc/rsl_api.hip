@@ -410,7 +410,9 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   return hip_check(h,
                    rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
                                         (const long long*)ncell_dev, ncell, (const float*)steer_tab, ntiles, G,
-                                        music, (int*)out_idx, (float*)out_gmax, (float*)out_spec, (int)blocks),
+                                        music, (int*)out_idx, (float*)out_gmax, (float*)out_spec,
+                                        (method & RSL_DOA_SPEC_BLOCKED) ? 1 : (method & RSL_DOA_SPEC_GMAJOR) ? ncell : 0,
+                                        (int)blocks),
                    "doa_scan");
 }
 
@@ -666,4 +668,30 @@ int rsl_pose_rte(rsl_handle h, const void* aligned, const void* gt, long long n,
                                         (const double*)lengths, nlen, (double*)scratch, (double*)err,
                                         (unsigned long long*)counts, (double*)stats),
                    "pose_rte");
+}
+
+int rsl_music_subspace(rsl_handle h, const void* sigs, long long n, int M, int num_sources, const void* steer_c128,
+                       int G, void* spec) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 0 || M < 1 || M > 16 || G < 1) return fail(h, RSL_ERR_INVALID, "rsl_music_subspace: bad shape");
+  if (n == 0) return RSL_OK;
+  if (!sigs || !steer_c128 || !spec) return fail(h, RSL_ERR_INVALID, "rsl_music_subspace: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_music_subspace(h->stream, (const double*)sigs, n, M, num_sources,
+                                              (const double*)steer_c128, G, (double*)spec),
+                   "music_subspace");
+}
+
+int rsl_esprit_subspace(rsl_handle h, const void* sigs, long long n, int M, int num_sources, double esprit_scale,
+                        void* deg) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 0 || M < 1 || M > 16) return fail(h, RSL_ERR_INVALID, "rsl_esprit_subspace: bad shape");
+  if (n == 0) return RSL_OK;
+  if (!sigs || !deg) return fail(h, RSL_ERR_INVALID, "rsl_esprit_subspace: null pointer");
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_esprit_subspace(h->stream, (const double*)sigs, n, M, num_sources, esprit_scale,
+                                               (double*)deg),
+                   "esprit_subspace");
 }

@@ -61,9 +61,10 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const float4* __restrict__ steer, int ntiles, int G, int use_lds,
                                                   int* __restrict__ out_idx, float* __restrict__ out_gmax,
-                                                  float* __restrict__ out_spec) {
+                                                  float* __restrict__ out_spec, long long spec_ld) {
   constexpr int KSG = (KS + 3) / 4;
   extern __shared__ float4 sst[];
+  __shared__ float4 sstage[SPEC ? 4 * 64 : 1];  // per wave: one tile's 8 grid points x 32 cells (grid-major stores)
   const float4* st = steer;
   if (use_lds) {
     for (int x = threadIdx.x; x < ntiles * KSG * 64; x += 256) sst[x] = steer[x];
@@ -153,13 +154,40 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
             if constexpr (GMAX) bestg[t2] = gv;
           }
           if constexpr (SPEC) {
-            if (ok[t2] && g < G) {
-              float val = gv;
-              if constexpr (MUSIC) {
-                const float d = (pz[t2] > 0.f) ? Mf - gv : (Mf - 1.f);
-                val = (d > 1e-12f) ? 1.0f / d : 0.f;  // angle_estimation.py:149-152
-              }
+            float val = gv;
+            if constexpr (MUSIC) {
+              const float d = (pz[t2] > 0.f) ? Mf - gv : (Mf - 1.f);
+              val = (d > 1e-12f) ? __builtin_amdgcn_rcpf(d) : 0.f;  // angle_estimation.py:149-152 (v_rcp_f32: 1 ulp)
+            }
+            if (spec_ld > 0) {
+              // grid-major: stage the tile (8 grid points x 32 cells) in LDS, stored below as 128-B runs
+              reinterpret_cast<float*>(sstage + wave * 64)[(2 * q + h) * 32 + t2 * 16 + jj] = val;
+            } else if (ok[t2] && g < G) {  // cell-major [n][G] (the reference's per-target spectrum rows)
               out_spec[(size_t)cidx[t2] * G + g] = val;
+            }
+          }
+        }
+      }
+      if constexpr (SPEC) {
+        if (spec_ld > 0) {
+          __builtin_amdgcn_wave_barrier();
+          const int r = lane >> 3, c4 = lane & 7;  // grid point 8 t + r, cells 4 c4 .. 4 c4 + 3 of the chunk
+          const float4 v = sstage[wave * 64 + r * 8 + c4];
+          __builtin_amdgcn_wave_barrier();
+          const int g = 8 * t + r;
+          const long long c0 = ch * 32 + 4 * c4;
+          if (g < G && spec_ld == 1) {
+            // cell-blocked [ceil(n / 32)][G][32]: a tile is one contiguous 1 KiB run, a pass one 46 KiB block
+            *reinterpret_cast<float4*>(out_spec + ((size_t)ch * G + g) * 32 + 4 * c4) = v;
+          } else if (g < G) {
+            float* dst = out_spec + (size_t)g * spec_ld + c0;
+            if (c0 + 3 < ncell && (spec_ld & 3) == 0) {
+              *reinterpret_cast<float4*>(dst) = v;
+            } else {
+              if (c0 < ncell) dst[0] = v.x;
+              if (c0 + 1 < ncell) dst[1] = v.y;
+              if (c0 + 2 < ncell) dst[2] = v.z;
+              if (c0 + 3 < ncell) dst[3] = v.w;
             }
           }
         }
@@ -360,7 +388,7 @@ template <int KS, bool FAST, bool MUSIC, bool SPEC, bool GMAX>
 static hipError_t launch_scan_t(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                                 const int* c_rc, const long long* ncell_dev, long long ncell_host, const float4* stp,
                                 int ntiles, int G, int use_lds, size_t lds, int* out_idx, float* out_gmax,
-                                float* out_spec, int max_blocks) {
+                                float* out_spec, long long spec_ld, int max_blocks) {
   auto kern = k_doa_scan<KS, FAST, MUSIC, SPEC, GMAX>;
   static int per_cu[2] = {-1, -1};  // occupancy per CU for the LDS / no-LDS variants
   int& occ = per_cu[use_lds ? 1 : 0];
@@ -376,7 +404,7 @@ static hipError_t launch_scan_t(hipStream_t st, const float2* rds, int A, int S,
   if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
-                     ncell_host, stp, ntiles, G, use_lds, out_idx, out_gmax, out_spec);
+                     ncell_host, stp, ntiles, G, use_lds, out_idx, out_gmax, out_spec, spec_ld);
   return hipGetLastError();
 }
 
@@ -384,11 +412,11 @@ template <int KS, bool FAST>
 static hipError_t launch_scan_f(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                                 const int* c_rc, const long long* ncell_dev, long long ncell_host, const float4* stp,
                                 int ntiles, int G, int music, int use_lds, size_t lds, int* out_idx, float* out_gmax,
-                                float* out_spec, int max_blocks) {
+                                float* out_spec, long long spec_ld, int max_blocks) {
   const bool spec = out_spec != nullptr, gmax = out_gmax != nullptr;
 #define L(M, SP, GM)                                                                                               \
   return launch_scan_t<KS, FAST, M, SP, GM>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, \
-                                            use_lds, lds, out_idx, out_gmax, out_spec, max_blocks)
+                                            use_lds, lds, out_idx, out_gmax, out_spec, spec_ld, max_blocks)
   if (music) {
     if (spec) { if (gmax) L(true, true, true); else L(true, true, false); }
     else { if (gmax) L(true, false, true); else L(true, false, false); }
@@ -402,7 +430,7 @@ static hipError_t launch_scan_f(hipStream_t st, const float2* rds, int A, int S,
 hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,
                            int ntiles, int G, int music, int* out_idx, float* out_gmax, float* out_spec,
-                           int grid_blocks) {
+                           long long spec_ld, int grid_blocks) {
   const int KS = (2 * A + 3) / 4;
   const int KSG = (KS + 3) / 4;
   const size_t tab_bytes = (size_t)ntiles * KSG * 64 * sizeof(float4);
@@ -442,9 +470,10 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
   case n:                                                                                                          \
     if (fast && (n % 2 == 0))                                                                                      \
       return launch_scan_f<n, (n % 2 == 0)>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, \
-                                            music, use_lds, lds, out_idx, out_gmax, out_spec, grid_blocks);        \
+                                            music, use_lds, lds, out_idx, out_gmax, out_spec, spec_ld,             \
+                                            grid_blocks);                                                          \
     return launch_scan_f<n, false>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, stp, ntiles, G, music,   \
-                                   use_lds, lds, out_idx, out_gmax, out_spec, grid_blocks);
+                                   use_lds, lds, out_idx, out_gmax, out_spec, spec_ld, grid_blocks);
   switch (KS) {
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
     default:

@@ -62,7 +62,7 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
 hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const float* steer_tab,
                            int ntiles, int G, int music, int* out_idx, float* out_gmax, float* out_spec,
-                           int grid_blocks);
+                           long long spec_ld, int grid_blocks);
 // K5 fast path: Toeplitz-form argmax on f16 MFMA with hi/lo split (rsl_doa_toep.hip).
 hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
@@ -102,6 +102,11 @@ hipError_t launch_traj_apply(hipStream_t st, double* pos, double* quat, long F, 
 hipError_t launch_traj_stitch(hipStream_t st, const double* summ, int R, int rank, double dt, int method,
                               double* state, double* base);
 hipError_t launch_traj_smooth(hipStream_t st, const double* x, long F, int ncol, int size, double* out);
+// MUSIC / ESPRIT with num_sources != 1 (rsl_subspace.hip), fp64, per-call drop-in paths.
+hipError_t launch_music_subspace(hipStream_t st, const double* sigs, long n, int M, int K, const double* steer,
+                                 int G, double* spec);
+hipError_t launch_esprit_subspace(hipStream_t st, const double* sigs, long n, int M, int K, double esprit_scale,
+                                  double* deg);
 // Pose-error evaluation (rsl_eval.hip): Umeyama + quaternion-mean alignment, APE errors / statistics, RTE.
 long long pose_error_scratch_doubles(long long n, int nlen);
 hipError_t launch_pose_align(hipStream_t st, const double* est, const double* gt, long n, double* scratch,

@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get('RSL_LIBRARY', os.path.join(PKG_ROOT, 'lib', 'librsl.s
 RSL_OK, RSL_ERR_INVALID, RSL_ERR_UNSUPPORTED, RSL_ERR_HIP = 0, 1, 2, 3
 METHOD_BEAMFORMING, METHOD_MUSIC = 0, 1
 DOA_TOEPLITZ = 0x100
+DOA_SPEC_GMAJOR = 0x200
+DOA_SPEC_BLOCKED = 0x400
 STEER_TOEPLITZ = 1
 K_NAMES = ['range_fft', 'doppler_fft', 'detect', 'offsets', 'emit', 'doa_scan', 'cell_extras', 'confidence',
            'velocity', 'aux']
@@ -65,6 +67,8 @@ SIGNATURES = {
     'rsl_synth_pattern': (c_int, [_P, _P, c_int, c_int, c_int, c_double, c_double, c_double, c_double, _P]),
     'rsl_synth_cube': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_ulonglong, c_longlong, _P]),
     'rsl_pose_error_scratch_bytes': (c_longlong, [c_longlong, c_int]),
+    'rsl_music_subspace': (c_int, [_P, _P, c_longlong, c_int, c_int, _P, c_int, _P]),
+    'rsl_esprit_subspace': (c_int, [_P, _P, c_longlong, c_int, c_int, c_double, _P]),
     'rsl_pose_align': (c_int, [_P, _P, _P, c_longlong, _P, _P, _P, _P, _P]),
     'rsl_pose_rte': (c_int, [_P, _P, _P, c_longlong, _P, c_int, _P, _P, _P, _P]),
     'rsl_bvls': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, _P, _P, _P]),

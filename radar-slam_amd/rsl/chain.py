@@ -46,6 +46,9 @@ class ChainConfig:
     bounds: tuple = (-50.0, 50.0, -50.0, 50.0)
     entry_frac: float = 0.20                   # capacity: peak entries per cube cell (9.4 % measured)
     cell_frac: float = 1.00                    # capacity: unique cells per (range, doppler) cell (54-76 %)
+    spectrum: bool = False                     # also write the MUSIC / beamforming spectrum of every cell, f32
+                                               # cell-blocked [cells / 32, G, 32] (rsl.runtime.spectrum_rows)
+                                               # (angle_estimation.py:299 stores spectrum f64[G] per target)
 
     @property
     def S(self) -> int:
@@ -78,7 +81,7 @@ class RadarChain:
         self.k = 4 * np.pi * cfg.dt / lam_v
         self.method = _lib.METHOD_MUSIC if cfg.method == 'music' else _lib.METHOD_BEAMFORMING
         self.entry_cap = int(math.ceil(cfg.entry_frac * F * A * S * C)) + 64
-        self.cell_cap = int(math.ceil(cfg.cell_frac * F * S * C)) + 64
+        self.cell_cap = (int(math.ceil(cfg.cell_frac * F * S * C)) + 64 + 3) & ~3  # a multiple of 4 (16-B rows)
         e = ctx.empty
         W = (C + 63) // 64
         self.work = e((F, A, C, S), torch.complex64)
@@ -98,7 +101,8 @@ class RadarChain:
         self.vel = vel_out if vel_out is not None else e((F, 8), torch.float64)
         self.ncell_dev = self.offs['cell_base'][F:F + 1]
         # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
-        self.fused_doa = bool(self.steer['toeplitz']) and A >= 2
+        self.fused_doa = bool(self.steer['toeplitz']) and A >= 2 and not cfg.spectrum
+        self.spec = e(((self.cell_cap + 31) // 32, len(self.grid), 32), torch.float32) if cfg.spectrum else None
 
     def run(self, cube, *, esprit: bool = True, velocity: bool = True):
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""
@@ -142,9 +146,12 @@ class RadarChain:
                            esprit=self.ext['esprit'] if esprit else None, phase=self.ext['phase'] if velocity else None)
         else:
             ctx.doa(self.rds, L['c_frame'], L['c_rc'], self.steer, self.method, n=self.cell_cap,
-                    n_dev=self.ncell_dev, out_idx=self.gidx)
-            ctx.cell_extras(self.rds, L['c_frame'], L['c_rc'], n=self.cell_cap, n_dev=self.ncell_dev,
-                            esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity, bufs=self.ext)
+                    n_dev=self.ncell_dev, out_idx=self.gidx, want_spec=self.spec is not None, spec_blocked=True,
+                    out_spec=self.spec)
+            if esprit or velocity:
+                ctx.cell_extras(self.rds, L['c_frame'], L['c_rc'], n=self.cell_cap, n_dev=self.ncell_dev,
+                                esprit_scale=self.esprit_scale, want_esprit=esprit, want_phase=velocity,
+                                bufs=self.ext)
         if velocity:
             ctx.velocity(None, self.ext['phase'], self.offs['cell_base'], k=self.k, ridge=cfg.ridge,
                          bounds=cfg.bounds, amask=L['c_amask'], out=self.vel, gidx=self.gidx, az_table=self.az_table,

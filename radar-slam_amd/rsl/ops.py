@@ -148,6 +148,34 @@ def doa(method: str, steer_c128: np.ndarray, *, sigs=None, rds=None, rbins=None,
     return to_host(idx[:N]).astype(np.int64), (to_host(spec[:N], np.float64) if want_spec else None)
 
 
+def subspace_music(sigs, steer_c128: np.ndarray, num_sources: int, ctx: Optional[Context] = None) -> np.ndarray:
+    """MUSIC spectrum f64 [n, G] for any num_sources (angle_estimation.py:109-154; rsl_music_subspace)."""
+    c = _ctx(ctx)
+    s = np.ascontiguousarray(np.atleast_2d(np.asarray(sigs, dtype=np.complex128)))
+    st = np.ascontiguousarray(np.asarray(steer_c128, dtype=np.complex128))
+    n, M = s.shape
+    G = st.shape[0]
+    ds, dst = c.to_dev(s.view(np.float64)), c.to_dev(st.view(np.float64))
+    out = c.empty((n, G), c.torch.float64)
+    c._bind()
+    c.check(c.lib.rsl_music_subspace(c.h, _ptr(ds), n, M, int(num_sources), _ptr(dst), G, _ptr(out)),
+            'rsl_music_subspace')
+    return to_host(out)
+
+
+def subspace_esprit(sigs, num_sources: int, esprit_scale: float, ctx: Optional[Context] = None) -> np.ndarray:
+    """ESPRIT angles (deg) f64 [n] for any num_sources (angle_estimation.py:178-225; rsl_esprit_subspace)."""
+    c = _ctx(ctx)
+    s = np.ascontiguousarray(np.atleast_2d(np.asarray(sigs, dtype=np.complex128)))
+    n, M = s.shape
+    ds = c.to_dev(s.view(np.float64))
+    out = c.empty((n,), c.torch.float64)
+    c._bind()
+    c.check(c.lib.rsl_esprit_subspace(c.h, _ptr(ds), n, M, int(num_sources), float(esprit_scale), _ptr(out)),
+            'rsl_esprit_subspace')
+    return to_host(out)
+
+
 def cell_extras(*, sigs=None, rds=None, rbins=None, dbins=None, esprit_scale=1 / math.pi, want_sig=False,
                 want_esprit=False, want_phase=False, ctx: Optional[Context] = None):
     c = _ctx(ctx)

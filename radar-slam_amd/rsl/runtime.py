@@ -216,18 +216,29 @@ class Context:
 
     # -- a11-a16 ----------------------------------------------------------------------------------
     def doa(self, rds, c_frame, c_rc, steer, method: int, *, n: Optional[int] = None, n_dev=None,
-            want_gmax: bool = False, want_spec: bool = False, out_idx=None, fast: bool = True):
+            want_gmax: bool = False, want_spec: bool = False, out_idx=None, fast: bool = True,
+            spec_gmajor: bool = False, spec_blocked: bool = False, out_spec=None):
         """Steering-scan argmax per cell.  fast=True (default) uses the Toeplitz f16-MFMA path when the
         steering matrix is a uniform linear array and no spectrum is requested; fast=False forces the f32
-        [Re; Im] MFMA scan."""
+        [Re; Im] MFMA scan.  want_spec: the spectrum, f32 [n, G]; [G, n] (n = the capacity) with spec_gmajor;
+        [ceil(n / 32), G, 32] with spec_blocked (see spectrum_rows)."""
         torch = self.torch
         _, A, S, C = rds.shape
         cap = int(c_frame.shape[0]) if n is None else int(n)
         idx = out_idx if out_idx is not None else self.empty((max(cap, 1),), torch.int32)
         gmax = self.empty((max(cap, 1),), torch.float32) if want_gmax else None
-        spec = self.empty((max(cap, 1), steer['G']), torch.float32) if want_spec else None
+        spec = out_spec
+        if want_spec and spec is None:
+            G = steer['G']
+            shape = ((max(cap, 1) + 31) // 32, G, 32) if spec_blocked else (G, max(cap, 1)) if spec_gmajor else \
+                (max(cap, 1), G)
+            spec = self.empty(shape, torch.float32)
         self._bind()
         m = int(method)
+        if want_spec and spec_blocked:
+            m |= _lib.DOA_SPEC_BLOCKED
+        elif want_spec and spec_gmajor:
+            m |= _lib.DOA_SPEC_GMAJOR
         if fast and steer['toeplitz'] and not want_spec:
             m |= _lib.DOA_TOEPLITZ
         self.check(self.lib.rsl_doa(self.h, _ptr(rds), A, S, C, _ptr(c_frame), _ptr(c_rc), _ptr(n_dev), cap,
@@ -294,6 +305,12 @@ class Context:
 
 _ctx_lock = threading.Lock()
 _ctx: Dict[int, Context] = {}
+
+
+def spectrum_rows(spec_blocked, n: int):
+    """Cell-major [n, G] view (a device copy) of a cell-blocked spectrum [ceil(cap / 32), G, 32]."""
+    nb, G, _ = spec_blocked.shape
+    return spec_blocked.permute(0, 2, 1).reshape(nb * 32, G)[:n]
 
 
 def get_context(device: Optional[int] = None) -> Context:

@@ -7,8 +7,10 @@ The reference's MUSIC covariance is rank-1 (R = s s^H of one normalised snapshot
 noise-subspace denominator is M - |a^H s|^2 exactly and MUSIC shares beamforming's steering
 contraction |A^H S|^2; both run in librsl's MFMA scan kernel (``rsl_doa``).  ESPRIT's SVD of the
 (M-1)x2 shift matrix reduces to a 2x2 Hermitian eigenproblem, evaluated in fp64 (``rsl_cell_extras``).
-Only ``num_sources == 1`` (the reference's default and only call pattern) is supported: with a rank-1
-R any larger signal subspace is an arbitrary LAPACK null-space basis.
+``num_sources != 1`` runs the general subspace forms in fp64 (``rsl_music_subspace`` / ``rsl_esprit_subspace``):
+with a rank-1 R the reference's larger signal subspaces contain null-space vectors that LAPACK picks by round-off;
+the device fixes them by a Householder completion (see rsl_subspace.hip and tests/test_gpu_dropin.py for which
+outputs are reference-determined).
 """
 from __future__ import annotations
 
@@ -55,26 +57,25 @@ class AngleEstimator:
         return tables.steering_matrix([azimuth_deg], self.antenna_positions, self.lambda_c)[0]
 
     # -- a13 .. a16 -------------------------------------------------------------------------------------
-    @staticmethod
-    def _one_source(num_sources):
-        if num_sources != 1:
-            raise NotImplementedError("num_sources != 1: the rank-1 covariance has no defined multi-source "
-                                      "subspace (reference uses an arbitrary LAPACK null-space basis)")
-
     def music_spectrum(self, spatial_signature: np.ndarray, num_sources: int = 1) -> np.ndarray:
         """1/|a^H E_n E_n^H a| over the azimuth grid, 0 where <= 1e-12 (angle_estimation.py:109-154)."""
-        self._one_source(num_sources)
+        if num_sources != 1:
+            return ops.subspace_music(np.asarray(spatial_signature)[None], self._steer, num_sources)[0]
         _, spec = ops.doa('music', self._steer, sigs=np.asarray(spatial_signature)[None], want_spec=True)
         return spec[0]
 
     def estimate_angle_music(self, spatial_signature: np.ndarray, num_sources: int = 1) -> Tuple[float, np.ndarray]:
-        self._one_source(num_sources)
+        if num_sources != 1:
+            spec = self.music_spectrum(spatial_signature, num_sources)
+            return self.azimuth_grid[np.argmax(spec)], spec
         idx, spec = ops.doa('music', self._steer, sigs=np.asarray(spatial_signature)[None], want_spec=True)
         return self.azimuth_grid[idx[0]], spec[0]
 
     def estimate_angle_esprit(self, spatial_signature: np.ndarray, num_sources: int = 1) -> float:
         """Closed-form rank-1 ESPRIT in fp64 (angle_estimation.py:178-225); 0.0 if it fails, as the reference."""
-        self._one_source(num_sources)
+        if num_sources != 1:
+            return float(ops.subspace_esprit(np.asarray(spatial_signature)[None], num_sources,
+                                             self._esprit_scale)[0])
         try:
             _, esp, _ = ops.cell_extras(sigs=np.asarray(spatial_signature)[None], esprit_scale=self._esprit_scale,
                                         want_esprit=True)

@@ -127,8 +127,8 @@ def test_single_signature_methods(golden):
         assert abs(est.estimate_angle_esprit(s) - z['esprit_deg'][k]) < P.ESPRIT_TOL_DEG
         b, bspec = est.estimate_angle_beamforming(s)
         assert b == z['bf_deg'][k]
-    with pytest.raises(NotImplementedError):
-        est.music_spectrum(z['sig'][0], num_sources=2)
+    # num_sources != 1 runs (general subspace forms: test_music_num_sources_general / test_esprit_num_sources_general)
+    assert est.music_spectrum(z['sig'][0], num_sources=2).shape == (len(est.azimuth_grid),)
 
 
 @pytest.mark.parametrize('name', NAMES)
@@ -236,3 +236,81 @@ def test_robust_sequence_vs_golden(golden):
     st = rob.get_target_statistics()
     assert st['total_targets_tracked'] == int(z['stats'][0]) and st['active_targets'] == int(z['stats'][1])
     assert abs(st['average_confidence'] - z['stats'][2]) < 1e-5
+
+
+def _householder_den(s, a, K):
+    """numpy restatement of rsl_subspace.hip's basis: V = [s/|s|, Householder completion], den = sum_{noise j}
+    |(P a)_j|^2 (test side; the reference's null-space columns for 2 <= K < M are LAPACK round-off, parity unpinned)."""
+    M = len(s)
+    lo = (K if K < M else M) if K >= 0 else max(M + K, 0)
+    nx = np.linalg.norm(s)
+    if nx == 0:
+        return sum(abs(a[M - 1 - j]) ** 2 for j in range(lo, M))
+    ph = s[0] / abs(s[0]) if abs(s[0]) > 0 else 1.0
+    w = s.astype(complex).copy()
+    w[0] -= -ph * nx
+    pa = a - 2 * w * (np.vdot(w, a) / np.vdot(w, w).real)
+    return float(np.sum(np.abs(pa[lo:]) ** 2))
+
+
+def test_music_num_sources_general(ctx):
+    """num_sources != 1 (angle_estimation.py:109-176): K = 1 through the general path equals the closed form; K >= M
+    (no noise subspace) and zero signatures equal the reference's eigh outputs exactly (spectrum 0 / den = M - K);
+    K = 0 equals 1 / |a|^2; 2 <= K < M follows the Householder-basis definition and never lowers the spectrum
+    below K = 1's (den_K <= den_1)."""
+    from src.angle_estimation.angle_estimation import AngleEstimator
+    from rsl import ops
+    est = AngleEstimator()
+    grid, steer = est.azimuth_grid, est._steer
+    rs = np.random.RandomState(7)
+    sigs = rs.randn(6, 8) + 1j * rs.randn(6, 8)
+    sigs /= np.linalg.norm(sigs, axis=1, keepdims=True)
+    sigs[4] = steer[100] / np.sqrt(8)        # a pure steering vector: den -> 0 at grid point 100
+    sigs[5] = 0                               # zero power
+    closed = O.music_spectrum_closed(sigs[:5], steer)
+    g1 = ops.subspace_music(sigs[:5], steer, 1)
+    d1, dc = 1 / np.where(g1 > 0, g1, np.inf), 1 / np.where(closed > 0, closed, np.inf)
+    assert np.abs(d1 - dc).max() < 1e-12
+    for K in (8, 11):
+        assert (ops.subspace_music(sigs, steer, K) == 0).all()
+        ang, sp = est.estimate_angle_music(sigs[0], num_sources=K)
+        ref = O.music_spectrum_eigh(sigs[0], grid, num_sources=K)
+        assert ang == grid[np.argmax(ref)] == -90.0 and (sp == ref).all()
+    for K in (0, 2, 3, 7, -1, -3):
+        got = ops.subspace_music(sigs, steer, K)
+        zr = O.music_spectrum_eigh(sigs[5], grid, num_sources=K)  # zero signature: reference-determined
+        assert np.abs(got[5] - zr).max() < 1e-12, K
+        for n in range(5):
+            want = np.array([_householder_den(sigs[n], steer[g], K) for g in range(len(grid))])
+            live = want > 1e-9
+            assert (got[n][~live] == 0).all() or K <= 0, (K, n)  # den <= 1e-12 -> 0 (:149-152)
+            dg = 1 / got[n][live]
+            assert np.abs(dg - want[live]).max() < 1e-11 or K == 0, (K, n)
+            if K == 0:  # den = |a|^2 = M for every grid point (the reference's argmax is round-off)
+                assert np.abs(got[n] - 1 / 8).max() < 1e-12
+            if K >= 2:
+                assert (got[n] >= g1[min(n, 4)] * (1 - 1e-9)).all() if n < 5 else True
+
+
+def test_esprit_num_sources_general(ctx):
+    """ESPRIT num_sources != 1 (angle_estimation.py:178-225): K = 0 -> 0.0 (the reference's eigvals(empty)[0]
+    IndexError, caught); K = 1 equals the closed form; K = 2: the angle of one of the two eigenvalues of the
+    reference's Phi (which of the two is LAPACK's order: unpinned); K >= 3 runs (null-space columns: unpinned)."""
+    from src.angle_estimation.angle_estimation import AngleEstimator
+    from scipy.linalg import svd
+    est = AngleEstimator()
+    rs = np.random.RandomState(3)
+    lam = 3e8 / 77e9
+    for n in range(8):
+        s = np.exp(1j * np.arange(8) * rs.uniform(-2, 2)) + 0.3 * (rs.randn(8) + 1j * rs.randn(8))
+        s /= np.linalg.norm(s)
+        assert est.estimate_angle_esprit(s, num_sources=0) == 0.0 == O.esprit_svd(s, num_sources=0)
+        assert abs(est.estimate_angle_esprit(s, num_sources=1) - O.esprit_closed(s[None])[0]) < 1e-5  # fp32 path
+        U, _, _ = svd(np.column_stack([s[:-1], s[1:]]))
+        Phi = np.linalg.pinv(U[:-1, :2]) @ U[1:, :2]
+        cands = np.degrees(np.arcsin(np.angle(np.linalg.eigvals(Phi)) * lam / (2 * np.pi * (lam / 2))))
+        got = est.estimate_angle_esprit(s, num_sources=2)
+        assert np.min(np.abs(cands - got)) < 1e-7, (got, cands)
+        for K in (3, 5, 7, 9, -2):
+            v = est.estimate_angle_esprit(s, num_sources=K)
+            assert isinstance(v, float)

@@ -1,0 +1,87 @@
+"""Batched MUSIC / beamforming spectrum (configs[1]: "range-Doppler FFT + MUSIC spectrum"): RadarChain with
+spectrum=True writes f32 cell-blocked [cells / 32, G, 32] from the f32-MFMA steering scan (k_doa_scan,
+RSL_DOA_SPEC_BLOCKED).
+The reference stores spectrum f64[G] per target (angle_estimation.py:143-154, :299).
+
+Tolerance: MUSIC values are 1/den with den = M - |a^H s|^2 (rank-1 closed form); fp32 |a^H s|^2 from
+the fp32 RDS is good to ~1e-6 absolute, so the test compares den = 1/spectrum to the oracle's fp64 den within
+DEN_ATOL = 2e-5 (exact zeros where den <= 1e-12, which fp32 cannot reach for noise cells)."""
+import numpy as np
+import pytest
+
+import radar_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEN_ATOL = 2e-5
+
+
+def _frames(A, C, Tc, F, seed0=1000):
+    out = []
+    for f in range(F):
+        np.random.seed(seed0 + f)
+        out.append(O.synthesize_frame(O.TEST_SCENE, chirp_duration=Tc, num_chirps=C, num_antennas=A))
+    return np.stack(out)
+
+
+@pytest.mark.parametrize('name,A,C,Tc,method', [('cfg1', 8, 64, 25.6e-6, 'music'), ('cfg2', 8, 128, 51.2e-6, 'music'),
+                                               ('cfg1_bf', 8, 64, 25.6e-6, 'beamforming'),
+                                               ('a4', 4, 64, 25.6e-6, 'music')])
+def test_batched_spectrum_vs_oracle(ctx, name, A, C, Tc, method):
+    import rsl
+    F = 2
+    frames = _frames(A, C, Tc, F)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, spectrum=True, cell_frac=0.7,
+                          method=method)
+    ch = rsl.RadarChain(cfg, F, ctx)
+    ch.run(ctx.to_dev(frames.astype(np.complex64)), esprit=False, velocity=False)
+    res = ch.results()
+    nc = len(res['c_rc'])
+    from rsl.runtime import spectrum_rows
+    spec = spectrum_rows(ch.spec, nc).cpu().numpy()  # [cells, G]
+    grid = O.azimuth_grid()
+    steer = O.steering_matrix(grid, A)
+    cb = res['cell_base']
+    rs = np.random.RandomState(0)
+    for f in range(F):
+        ref = O.range_doppler_spectrum(frames[f], chirp_duration=Tc)
+        sl = np.arange(cb[f], cb[f + 1])
+        pick = sl if len(sl) <= 4000 else np.sort(rs.choice(sl, 4000, replace=False))
+        rc = res['c_rc'][pick]
+        sigs = np.stack([O.spatial_signature(ref, r // C, r % C) for r in rc])
+        got = spec[pick]
+        # the scan's argmax is a maximum of the written spectrum (1/(M - g) in fp32 can tie two close g values)
+        n = np.arange(len(pick))
+        assert (got[n, res['gidx'][pick]] == got.max(axis=1)).all()
+        if method == 'music':
+            want = O.music_spectrum_closed(sigs, steer)
+            assert ((got > 0) == (want > 0)).all()
+            dg = np.where(got > 0, 1.0 / np.where(got > 0, got, 1.0), 0.0)
+            dw = np.where(want > 0, 1.0 / np.where(want > 0, want, 1.0), 0.0)
+            err = np.abs(dg - dw).max()
+        else:
+            want = O.beamforming_spectrum(sigs, steer)
+            err = np.abs(got - want).max()
+        print(f'{name} frame {f}: {len(pick)} cells, max |den - den_ref| = {err:.2e}')
+        assert err < DEN_ATOL, (name, f, err)
+
+
+def test_spectrum_layouts_agree(ctx):
+    """Grid-major (RSL_DOA_SPEC_GMAJOR), cell-blocked (RSL_DOA_SPEC_BLOCKED) and cell-major spectra of the same cells
+    are bit-identical."""
+    import rsl
+    import torch
+    frames = _frames(8, 64, 25.6e-6, 1)
+    cfg = rsl.ChainConfig(num_antennas=8, num_chirps=64, chirp_duration=25.6e-6)
+    ch = rsl.RadarChain(cfg, 1, ctx)
+    ch.run(ctx.to_dev(frames.astype(np.complex64)))
+    nc = ch.totals()[1]
+    L = ch.lists
+    _, _, s_cm = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True)
+    _, _, s_gm = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
+                         spec_gmajor=True)
+    _, _, s_bl = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
+                         spec_blocked=True)
+    from rsl.runtime import spectrum_rows
+    torch.cuda.synchronize()
+    assert torch.equal(s_cm, s_gm.t())
+    assert torch.equal(s_cm, spectrum_rows(s_bl, nc))
