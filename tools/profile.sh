@@ -4,7 +4,7 @@
 # 1) kernel trace + stats of bench.py, 2) FETCH_SIZE pass, 3) WRITE_SIZE pass, 4) MFMA/VALU busy pass,
 # then tools/pmc_summary.py -> profiles/TAG_pmc.json and the stats CSV -> profiles/TAG_kernel_stats.csv.
 set -euo pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
