@@ -226,6 +226,18 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   bool sup = true;
   int group = 1;
   hipError_t e;
+  if (!db_map && rsl::rds_ring_supported(C, S) && getenv("RSL_RING") && atoi(getenv("RSL_RING")) != 0) {
+    {
+      Scope sc(h, RSL_K_RANGE_FFT);
+      e = rsl::launch_rds_ring(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
+                               tC, dc_removal, (float2*)work, (float2*)rds, thr_power, i_lo, i_hi,
+                               (unsigned long long*)mask, (int*)row_count, (float*)peak_pow, &group, &sup);
+    }
+    if (sup) {
+      if (peak_pow_group) *peak_pow_group = group;
+      return hip_check(h, e, "rds_ring");
+    }
+  }
   if (!db_map && rsl::rds_fused_supported(C, S)) {  // one pass over the cube; `work` holds the Doppler 3-max
     {
       Scope sc(h, RSL_K_RANGE_FFT);
@@ -635,6 +647,13 @@ int rsl_synth_cube(rsl_handle h, const void* pattern, int F, int A, int C, int S
                    rsl::launch_synth_cube(h->stream, (const double2*)pattern, F, A, C, S, noise_power, seed, frame0,
                                           (float2*)cube),
                    "synth_cube");
+}
+
+long long rsl_ring_faults(rsl_handle h) {
+  if (!h) return -1;
+  hipSetDevice(h->device);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return (long long)rsl::ring_faults();
 }
 
 long long rsl_pose_error_scratch_bytes(long long n, int nlen) {

@@ -1048,4 +1048,329 @@ hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K12 ring: range FFT and Doppler FFT + detection in ONE persistent launch, with the `work` intermediate kept in the
+// XCD's L2 instead of making an HBM round trip (8.4 MB per cfg2 frame written by K1 and read back by K2).
+//
+// A slab (frame, antenna) is the transpose unit: its C x S range spectra (512 KiB at cfg2) are produced by NP = C / CB
+// range tiles (K1's body: CB chirps x S) and consumed by NC = S / KB Doppler tiles (K2's body: KB range bins x C
+// chirps + 2 halo bins).  Every XCD owns the slabs s = x + 8 k of the launch (x = the XCD's HW_REG_XCC_ID) and a ring
+// of R slab buffers at the front of `work`, and its workgroups dequeue that XCD's items in the order
+//     P(0) .. P(L-1) | C(0) P(L) | C(1) P(L+1) | ...      (P(k): the NP range tiles of slab k, C(k): its NC tiles)
+// so a slab's range spectra are produced L slabs ahead of their Doppler tiles.  Hand-offs stay inside one XCD's L2:
+//   - a range tile stores its rows (plain stores: the lines stay in L2), waits vmcnt(0) in every wave, and after a
+//     workgroup barrier one lane adds 1 to prod[x][k % R];
+//   - a Doppler tile polls prod[x][k % R] >= NP (k / R + 1) with an L2-served (sc1) load, then loads its rows with
+//     L1-bypassing (nt) loads, so no L1 line of an earlier use of the ring slot can be read; after the rows are in LDS
+//     one lane adds 1 to cons[x][k % R];
+//   - the range tiles of slab k >= R wait for cons[x][k % R] >= NC (k / R) (the slot's previous slab fully read).
+// Counters only grow within a launch (uses of a slot are ordered by those waits) and the last workgroup to leave
+// resets the launch slot.  Every dependency points to an item dequeued earlier, and an item is dequeued only by a
+// running workgroup, so the smallest unfinished item can always run: no residency assumption, no deadlock.  The
+// queues are chosen by the XCD each workgroup actually runs on (HW_REG_XCC_ID), so producer and consumer of a slab
+// always share an L2 whatever the placement; the host enables the path only on an 8-XCC device.
+//
+// Measured (tools/ring_ab.py, 2000 cfg2 frames, outputs bit-identical to K1 + K2): 7.4-7.5 ms per launch at R 6, L 5
+// vs 6.7-6.9 ms for K1 + K2 in the same processes, so the path is opt-in (RSL_RING=1).  The hand-off itself is cheap
+// (waits ~5 % of workgroup time, RSL_RING_PROF) and keeping the slabs in L2 barely matters (own-address slabs, no
+// reuse: 7.9 ms); the launch is bound by its single register / LDS budget: the range role needs 157 VGPRs and 42 KiB
+// of LDS, which caps the Doppler role at 3 workgroups per CU where K2 alone runs 7 (a Doppler tile takes 7.4 us here;
+// two tiles per item with both loads in flight need 187 VGPRs: 9.5 ms).
+// ---------------------------------------------------------------------------------------------
+constexpr int kRingSlots = 8;  // launches in flight (round-robin, as K1's queues)
+constexpr int kRingMaxR = 16;  // ring slabs per XCD (counter slots)
+struct RingSync {
+  unsigned head[8][32];                 // per-XCD dequeue heads (each counter on its own 128-B line)
+  unsigned prod[8][kRingMaxR][32];      // range tiles finished, per (XCD, ring slot)
+  unsigned cons[8][kRingMaxR][32];      // Doppler tiles that have read their rows, per (XCD, ring slot)
+  unsigned exit_[32];                   // workgroups that have left
+};
+__device__ RingSync g_ring[kRingSlots];
+__device__ unsigned g_ring_faults;  // launches that left a queue undrained, or whose waits timed out
+__device__ unsigned long long g_ring_prof[8];  // RSL_RING_PROF: clock sums over workgroups (A/B diagnostics)
+
+unsigned ring_faults() {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ring_faults), sizeof(v)) != hipSuccess) return ~0u;
+  return v;
+}
+
+RSL_DEV unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 7u;
+}
+
+RSL_DEV unsigned ld_relaxed(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane waits for *p >= target (bounded: ~2 s of polling, then the launch goes on and the outputs are wrong rather
+// than the GPU hung); the caller's barrier broadcasts the wait.
+RSL_DEV void ring_wait(const unsigned* p, unsigned target) {
+  unsigned it = 0;
+  for (; ld_relaxed(p) < target && it < (1u << 21); ++it) __builtin_amdgcn_s_sleep(8);
+  if (it == (1u << 21)) atomicAdd(&g_ring_faults, 1u);
+}
+
+template <int S, int C, int CB, int KB, int WPE = 0, int CT = 1>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void k_rds_ring(const float2* __restrict__ cube, int A, int Ct, int c0,
+                                                      long nfa, const float2* __restrict__ table,
+                                                      const float2* __restrict__ twS, const float2* __restrict__ twC,
+                                                      int dc, float2* __restrict__ work, int R, int L, int ring, int Q,
+                                                      float2* __restrict__ rds, float thr_f, int i_lo, int i_hi,
+                                                      unsigned long long* __restrict__ mask, int* __restrict__ row_count,
+                                                      float* __restrict__ pk_pow, int slot, int prof) {
+  constexpr int NT = kThreads;
+  constexpr int NP = C / CB, NC = S / KB / CT;  // items per slab
+  unsigned long long t_all = prof ? clock64() : 0, t_p = 0, t_c = 0, w_p = 0, w_c = 0, n_p = 0, n_c = 0;
+  constexpr int LDS_S = lp_row(S);         // range rows (padded)
+  constexpr int H = S / 2;
+  constexpr int PF = CB * H / NT;          // float4 per thread per range tile
+  constexpr int NR = KB + 2;
+  constexpr int LDC = lp_row(C) | 1;       // Doppler rows (padded, odd)
+  constexpr int CS = NT / KB, PI = C / CS, PH = (2 * C + NT - 1) / NT;
+  static_assert(C % CB == 0 && S % KB == 0 && (S / 2) % KB == 0 && (S / KB) % CT == 0, "tiles must divide the slab");
+  static_assert((CB * H) % NT == 0 && NT % KB == 0 && C % CS == 0 && CS % 8 == 0, "tile maps");
+  static_assert(dd_reg_ok<C, KB, NT>(), "register Doppler body");
+  extern __shared__ float2 sm[];
+  float2* tS = sm;                 // S twiddles at padded positions
+  float2* tC = sm + LDS_S;         // C twiddles
+  float2* buf = tC + C;            // range tile [CB][LDS_S] or Doppler tile [NR][LDC] + exchange words
+  __shared__ unsigned s_next;
+  const int tid = threadIdx.x;
+  for (int k = tid; k < S; k += NT) tS[lp(k)] = twS[k];
+  for (int k = tid; k < C; k += NT) tC[k] = twC[k];
+  const unsigned x = xcc_id();
+  RingSync& sy = g_ring[slot];
+  const unsigned nk = nfa > (long)x ? (unsigned)((nfa - (long)x + 7) / 8) : 0u;  // slabs of this XCD
+  const unsigned total = nk * (NP + NC);
+  const unsigned Lp = (unsigned)L < nk ? (unsigned)L : nk;
+  const unsigned nfull = nk > (unsigned)L ? nk - (unsigned)L : 0u;
+  const float4* tab4 = reinterpret_cast<const float4*>(table);
+  const size_t slab = (size_t)C * S;
+  unsigned* head = &sy.head[x][0];
+  // the queue hands out runs of Q consecutive items (one atomic per run); the next run is claimed one ahead
+  unsigned claim = 0;
+  if (tid == 0) s_next = atomicAdd(head, 1u);
+  __syncthreads();
+  unsigned run = __builtin_amdgcn_readfirstlane(s_next);
+  while (run * (unsigned)Q < total) {
+    if (tid == 0) claim = atomicAdd(head, 1u);
+    const unsigned iend = min(total, (run + 1) * (unsigned)Q);
+    for (unsigned it = run * (unsigned)Q; it < iend; ++it) {
+    // decode: role, slab k of this XCD, tile j
+    bool prod_role;
+    unsigned k, j;
+    if (it < Lp * NP) {
+      prod_role = true; k = it / NP; j = it % NP;
+    } else {
+      const unsigned m = it - Lp * NP;
+      if (m < nfull * (NP + NC)) {
+        const unsigned b = m / (NP + NC), q = m % (NP + NC);
+        if (q < NC) { prod_role = false; k = b; j = q; }
+        else { prod_role = true; k = b + (unsigned)L; j = q - NC; }
+      } else {
+        const unsigned m2 = m - nfull * (NP + NC);
+        prod_role = false; k = nfull + m2 / NC; j = m2 % NC;
+      }
+    }
+    const unsigned r = k % (unsigned)R, use = k / (unsigned)R;
+    const long fa = (long)x + 8L * k;
+    float2* wslab = work + (ring ? (size_t)(x * (unsigned)R + r) : (size_t)fa) * slab;
+    const unsigned long long t0 = prof ? clock64() : 0;
+    if (prod_role) {
+      // ---- range tile: chirps j CB .. j CB + CB - 1 of slab fa (K1's body) ----
+      const float4* src4 = reinterpret_cast<const float4*>(cube + ((size_t)fa * Ct + c0 + j * CB) * S);
+      float4 nx[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) nx[q] = ld16<true>(src4 + tid + q * NT);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int idx = tid + q * NT;
+        const int rr = idx / H, s2 = idx - rr * H;
+        const float4 tb = tab4[s2];
+        buf[rr * LDS_S + lp(2 * s2)] = cmul(make_float2(nx[q].x, nx[q].y), make_float2(tb.x, tb.y));
+        buf[rr * LDS_S + lp(2 * s2 + 1)] = cmul(make_float2(nx[q].z, nx[q].w), make_float2(tb.z, tb.w));
+      }
+      __syncthreads();
+      fft_rows<S, CB, NT, LDS_S, true>(buf, tS, tid);
+      if (dc) {
+        if (tid < CB) buf[tid * LDS_S] = make_float2(0.f, 0.f);
+      }
+      const unsigned long long tw0 = prof ? clock64() : 0;
+      if (tid == 0 && use > 0) ring_wait(&sy.cons[x][r][0], (unsigned)NC * use);  // the slot's previous slab is read
+      __syncthreads();
+      if (prof) w_p += clock64() - tw0;
+      float4* dst4 = reinterpret_cast<float4*>(wslab + (size_t)j * CB * S);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int idx = tid + q * NT;
+        const int rr = idx / H, s2 = idx - rr * H;
+        const float2 lo = buf[rr * LDS_S + lp(2 * s2)], hi = buf[rr * LDS_S + lp(2 * s2 + 1)];
+        dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);  // plain stores: the lines stay in this XCD's L2
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) atomicAdd(&sy.prod[x][r][0], 1u);
+      if (prof) { t_p += clock64() - t0; ++n_p; }
+    } else {
+      // ---- Doppler item: CT tiles of KB range bins (+ halo) of slab fa (K2's body); the loads of all CT tiles are in
+      // flight together (memory-level parallelism at the kernel's low occupancy) ----
+      if (tid == 0) ring_wait(&sy.prod[x][r][0], (unsigned)NP * (use + 1));
+      __syncthreads();
+      if (prof) w_c += clock64() - t0;
+      const int ri = tid % KB, cs = tid / KB;
+      float2 ld[CT][PI + PH];
+#pragma unroll
+      for (int u = 0; u < CT; ++u) {
+        const int k0 = (int)(j * CT + u) * KB;
+        const float2* p = wslab + (unsigned)(cs * S + k0 + ri);
+#pragma unroll
+        for (int q = 0; q < PI; ++q) ld[u][q] = ld8<true>(p + (unsigned)(q * CS * S));
+        int kl = k0 - 1, kh = k0 + KB;
+        if (kl < 0) kl += S;
+        if (kh >= S) kh -= S;
+#pragma unroll
+        for (int h = 0; h < PH; ++h) {
+          const int e = tid + h * NT;
+          if ((2 * C) % NT == 0 || e < 2 * C) {
+            const int side = e / C, c = e - side * C;
+            ld[u][PI + h] = ld8<true>(wslab + (unsigned)(c * S + (side ? kh : kl)));
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CT; ++u) {
+        const int k0 = (int)(j * CT + u) * KB;
+        float2* row = buf + (ri + 1) * LDC + lp(cs);
+#pragma unroll
+        for (int q = 0; q < PI; ++q) row[lp(q * CS)] = ld[u][q];
+#pragma unroll
+        for (int h = 0; h < PH; ++h) {
+          const int e = tid + h * NT;
+          if ((2 * C) % NT == 0 || e < 2 * C) {
+            const int side = e / C, c = e - side * C;
+            buf[(side ? NR - 1 : 0) * LDC + lp(c)] = ld[u][PI + h];
+          }
+        }
+        if (u == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every tile's rows are in registers
+        __syncthreads();
+        if (u == 0 && tid == 0) atomicAdd(&sy.cons[x][r][0], 1u);  // the slot may be refilled
+        fft_rows<C, NR, NT, LDC, false, true>(buf, tC, tid);
+        dd_tile_compute_reg<C, KB, NT, 0, 10>(buf, reinterpret_cast<float*>(buf + NR * LDC), S, k0, (unsigned)fa, rds,
+                                              thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow);
+        __syncthreads();
+      }
+      if (prof) { t_c += clock64() - t0; ++n_c; }
+    }
+    }
+    if (tid == 0) s_next = claim;
+    __syncthreads();
+    run = __builtin_amdgcn_readfirstlane(s_next);
+  }
+  if (prof && tid == 0) {
+    const unsigned long long v[7] = {clock64() - t_all, t_p, t_c, w_p, w_c, n_p, n_c};
+    for (int q = 0; q < 7; ++q) atomicAdd(&g_ring_prof[q], v[q]);
+  }
+  // every claim of this workgroup has returned; the last workgroup to leave checks that every XCD's queue was
+  // drained (an XCD without workgroups would leave its slabs unprocessed: counted in g_ring_faults) and resets the
+  // launch slot
+  if (tid == 0 && atomicAdd(&sy.exit_[0], 1u) == gridDim.x - 1u) {
+    for (int q = 0; q < 8; ++q) {
+      const unsigned nq = nfa > (long)q ? (unsigned)((nfa - (long)q + 7) / 8) : 0u;
+      if (ld_relaxed(&sy.head[q][0]) * (unsigned)Q < nq * (NP + NC)) atomicAdd(&g_ring_faults, 1u);  // NC: items
+    }
+    for (int q = 0; q < 8; ++q) {
+      atomicExch(&sy.head[q][0], 0u);
+      for (int rr = 0; rr < kRingMaxR; ++rr) {
+        atomicExch(&sy.prod[q][rr][0], 0u);
+        atomicExch(&sy.cons[q][rr][0], 0u);
+      }
+    }
+    atomicExch(&sy.exit_[0], 0u);
+    if (prof) {
+      unsigned long long v[7];
+      for (int q = 0; q < 7; ++q) v[q] = atomicExch(&g_ring_prof[q], 0ull);
+      printf("RINGPROF grid %u all %llu p %llu c %llu wait_p %llu wait_c %llu n_p %llu n_c %llu\n", gridDim.x, v[0],
+             v[1], v[2], v[3], v[4], v[5], v[6]);
+    }
+  }
+}
+
+// Device check for the ring path: 8 XCCs (the queues are indexed by HW_REG_XCC_ID & 7).
+static bool ring_device_ok() {
+  static int ok = -1;
+  if (ok < 0) {
+    int dev = 0, nx = 0;
+    (void)hipGetDevice(&dev);
+    ok = (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) == hipSuccess && nx == 8) ? 1 : 0;
+  }
+  return ok == 1;
+}
+
+bool rds_ring_supported(int C, int S) { return C == 128 && S == 512; }
+
+// RSL_RING_R / RSL_RING_L: ring slabs per XCD and lead (slabs); RSL_RING_BPC: workgroups per CU; RSL_RING_Q: items per
+// dequeue; RSL_RING_PROF: clock breakdown printed by the last workgroup (A/B diagnostics)
+template <int CB, int WPE, int CT>
+static hipError_t launch_rds_ring_t(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0,
+                                    const float2* table, const float2* twS, const float2* twC, int dc, float2* work,
+                                    float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
+                                    int* row_count, float* pk_pow, int* pk_group) {
+  constexpr int SS = 512, CC = 128, KB = 16;
+  auto kern = k_rds_ring<SS, CC, CB, KB, WPE, CT>;
+  constexpr int LDS_S = lp_row(SS), NR = KB + 2, LDC = lp_row(CC) | 1;
+  constexpr int BUF = (CB * LDS_S > NR * LDC + KB * (CC / 64) * 2) ? CB * LDS_S : NR * LDC + KB * (CC / 64) * 2;
+  const size_t lds = sizeof(float2) * (size_t)(LDS_S + CC + BUF);
+  const long nfa = (long)F * A;
+  int R = 6, L = 5;  // fastest measured (tools/ring_ab.py)
+  if (const char* e = getenv("RSL_RING_R")) R = atoi(e);
+  if (const char* e = getenv("RSL_RING_L")) L = atoi(e);
+  // a Doppler tile may only wait for items dequeued before it (L >= 1), and a range tile only for the slot's previous
+  // slab (L < R): then the smallest unfinished item can always run
+  if (R < 2) R = 2;
+  if (R > kRingMaxR) R = kRingMaxR;
+  if (L < 1) L = 1;
+  // a batch smaller than the ring (or RSL_RING_OWN=1, A/B) uses its own slab addresses; the slot waits stay (they
+  // keep the per-slot counters exact)
+  int ring = nfa >= 8L * R ? 1 : 0;
+  if (const char* e = getenv("RSL_RING_OWN"))
+    if (atoi(e) != 0) ring = 0;
+  if (L > R - 1) L = R - 1;
+  const int prof = getenv("RSL_RING_PROF") ? 1 : 0;
+  int Q = 1;  // items per dequeue
+  if (const char* e = getenv("RSL_RING_Q")) Q = atoi(e) < 1 ? 1 : (atoi(e) > 16 ? 16 : atoi(e));
+  int nb = 0, dev = 0, ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kThreads, lds) != hipSuccess || nb < 1) nb = 1;
+  if (nb > 8) nb = 8;
+  if (const char* e = getenv("RSL_RING_BPC"))
+    if (atoi(e) > 0 && atoi(e) < nb) nb = atoi(e);
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // the whole chip (every XCD needs workgroups for its queue; extra ones leave at once)
+  const long grid = (long)nb * ncu;
+  static std::atomic<int> next_slot{0};
+  const int slot = next_slot.fetch_add(1) % kRingSlots;
+  *pk_group = KB;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, st, cube, A, Ct, c0, nfa, table, twS, twC, dc,
+                     work, R, L, ring, Q, rds, threshold_as_float(thr_p), i_lo, i_hi, mask, row_count, pk_pow, slot, prof);
+  return hipGetLastError();
+}
+
+hipError_t launch_rds_ring(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
+                           const float2* table, const float2* twS, const float2* twC, int dc, float2* work,
+                           float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
+                           float* pk_pow, int* pk_group, bool* supported) {
+  *supported = rds_ring_supported(C, S) && ring_device_ok();
+  if (!*supported || F <= 0) return hipSuccess;
+  const char* e = getenv("RSL_RING_CT");  // Doppler tiles per item (1 or 2; A/B)
+  if (e && atoi(e) == 2)
+    return launch_rds_ring_t<8, 0, 2>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi,
+                                      mask, row_count, pk_pow, pk_group);
+  return launch_rds_ring_t<8, 0, 1>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi, mask,
+                                    row_count, pk_pow, pk_group);
+}
+
 }  // namespace rsl

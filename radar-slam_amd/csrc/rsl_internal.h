@@ -33,6 +33,15 @@ hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int 
 // of detection (Doppler 3-max + candidate bits into `work`), then the range-direction finish -> the same mask /
 // row_count / tile-compact peak powers as launch_doppler_detect.  S = 512, C = 128; opt-in with RSL_FUSED=1 (slower).
 bool rds_fused_supported(int C, int S);
+// K1 + K2 in one persistent launch with `work` as a per-XCD ring of slabs held in L2 (rsl_fft.hip; S = 512, C = 128,
+// an 8-XCC device).  Outputs as launch_doppler_detect (tile-compact peak powers, group KB).  ring_faults(): launches
+// that left a queue undrained or timed out a wait (0 on a healthy run).
+bool rds_ring_supported(int C, int S);
+hipError_t launch_rds_ring(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
+                           const float2* table, const float2* twS, const float2* twC, int dc, float2* work,
+                           float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
+                           float* pk_pow, int* pk_group, bool* supported);
+unsigned ring_faults();
 hipError_t launch_rds_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
                             const float2* table, const float2* tw_S, const float2* tw_C, int dc, float2* rds,
                             void* work, double thr_p, int i_lo, int i_hi);
