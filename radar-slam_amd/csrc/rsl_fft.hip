@@ -576,7 +576,47 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   // (one address add per load, 128-B aligned row segments), then the two halo rows spread over all threads
   constexpr int CS = NT / KB;
   constexpr bool STRUCT = (NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16);
-  if constexpr (STRUCT) {
+  // CP bit 5: interior rows as 16-B loads (a lane reads two adjacent range bins of one chirp: half the load
+  // instructions); thread = (bin pair rp, chirp slot cs2), chirps cs2 + CS2 q
+  constexpr int CS2 = NT / (KB / 2);
+  constexpr bool WIDE = ((CP & 32) != 0) && (KB % 2 == 0) && (NT % (KB / 2) == 0) && (C % CS2 == 0);
+  if constexpr (WIDE) {
+    constexpr int PI = C / CS2, PH = (2 * C + NT - 1) / NT;
+    const int rp = tid % (KB / 2), cs = tid / (KB / 2);
+    float4 ld[PI];
+    float2 lh[PH];
+    const float4* p = reinterpret_cast<const float4*>(src + (unsigned)(cs * S + k0 + 2 * rp));
+#pragma unroll
+    for (int q = 0; q < PI; ++q) ld[q] = p[(unsigned)(q * CS2 * S / 2)];
+    int kl = k0 - 1, kh = k0 + KB;
+    if (kl < 0) kl += S;
+    if (kh >= S) kh -= S;
+#pragma unroll
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        lh[h] = src[(unsigned)(c * S + (side ? kh : kl))];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TWP; ++q)
+      if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+    float2* row0 = buf + (2 * rp + 1) * LD + lpp<PAD>(cs);
+#pragma unroll
+    for (int q = 0; q < PI; ++q) {
+      row0[lpp<PAD>(q * CS2)] = make_float2(ld[q].x, ld[q].y);
+      row0[LD + lpp<PAD>(q * CS2)] = make_float2(ld[q].z, ld[q].w);
+    }
+#pragma unroll
+    for (int h = 0; h < PH; ++h) {
+      const int e = tid + h * NT;
+      if ((2 * C) % NT == 0 || e < 2 * C) {
+        const int side = e / C, c = e - side * C;
+        buf[(side ? NR - 1 : 0) * LD + lpp<PAD>(c)] = lh[h];
+      }
+    }
+  } else if constexpr (STRUCT) {
     constexpr int PI = C / CS, PH = (2 * C + NT - 1) / NT;
     const int ri = tid % KB, cs = tid / KB;
     float2 ld[PI + PH];
@@ -771,6 +811,7 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
       if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 0, 7>;
       if (v == 10) kern = k_doppler_detect<C, KB, NT, true, 0, 10>;
       if (v == 26) kern = k_doppler_detect<C, KB, NT, true, 0, 26>;
+      if (v == 42) kern = k_doppler_detect<C, KB, NT, true, 0, 42>;  // 10 + 16-B interior loads
     }
   }
   if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {
