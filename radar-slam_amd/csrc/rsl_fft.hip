@@ -413,10 +413,11 @@ template <int C, int KB, int NT, int DBG = 0, int CP = 0>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
                                  int* __restrict__ row_count, float* __restrict__ dbmap,
-                                 float* __restrict__ pk_pow) {
+                                 float* __restrict__ pk_pow, int tid_in = -1) {
   constexpr int LD = lp_row(C) | 1;
   constexpr int NCH = C / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // tid_in: a laundered thread index from a persistent caller (keeps per-thread addresses out of its tile loop)
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = wave % NCH, rh = wave / NCH;
   const int j = ch * 64 + lane;  // shifted Doppler column: out[j] = X[(j - C//2) mod C]
   int d = j - C / 2;
@@ -757,8 +758,19 @@ __global__ __launch_bounds__(NT) void k_doppler_detect_p(const float2* __restric
     __syncthreads();
     if (t + nb8 < hi) issue(t + nb8);  // in flight during this tile's FFT, stores and detection
     const int kb = (int)((unsigned)t % nkb);
-    dd_tile_compute<C, KB, NT, true, 0>(buf, tws, S, kb * KB, (unsigned)t / nkb, rds, thr_f, i_lo, i_hi, mask,
-                                        row_count, dbmap, pk_pow);
+    if constexpr (dd_reg_ok<C, KB, NT>()) {  // the register body (tile-compact peak powers, as K2)
+      // a laundered thread index: the per-thread LDS addresses of the FFT stages and the detection are recomputed
+      // per tile instead of being hoisted out of the loop (held across tiles they cost ~70 VGPRs)
+      int tl = tid;
+      asm volatile("" : "+v"(tl));
+      fft_rows<C, NR, NT, LD, false, true>(buf, tws, tl);
+      dd_tile_compute_reg<C, KB, NT, 0, 10>(buf, reinterpret_cast<float*>(buf + NR * LD), S, kb * KB,
+                                            (unsigned)t / nkb, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap,
+                                            pk_pow, tl);
+    } else {
+      dd_tile_compute<C, KB, NT, true, 0>(buf, tws, S, kb * KB, (unsigned)t / nkb, rds, thr_f, i_lo, i_hi, mask,
+                                          row_count, dbmap, pk_pow);
+    }
     __syncthreads();  // the detection reads the LDS tile; the next tile's staging overwrites it
   }
 }
@@ -785,7 +797,9 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
     if ((size_t)atol(e) > lds) lds = (size_t)atol(e);
   const float thr_f = threshold_as_float(thr_p);
   // one tile per workgroup: a persistent variant with a register prefetch of the next tile measured slower
-  // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy)
+  // (4.7 vs 3.2 ms per 1000 cfg2 frames; the prefetch registers cost occupancy); rebuilt on the register tile body
+  // with a laundered thread index (93 VGPRs, 5 workgroups per CU): still 5.0-5.25 vs 3.85 ms per 2000 frames
+  // (tools/ring_ab.py, RSL_DD_PERSIST=1; outputs bit-identical)
   // 256 threads (a 320-thread block that runs each radix-8 stage of the 18-row KB-16 tile in one pass measured
   // slower: 2.72 vs 2.48 ms per 1000 cfg2 frames)
   constexpr int NT = 256;
@@ -820,6 +834,7 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
       auto pk = k_doppler_detect_p<C, KB, NT>;
       long nblk = resident_grid(reinterpret_cast<const void*>(pk), lds, ntile) & ~7L;
       if (nblk >= 8) {
+        if (dd_reg_ok<C, KB, NT>()) *pk_group = KB;
         hipLaunchKernelGGL(pk, dim3((unsigned)nblk), dim3(NT), lds, st, work, S, tw, rds, thr_f, i_lo, i_hi, mask,
                            row_count, dbmap, pk_pow, ntile);
         return hipGetLastError();

@@ -56,6 +56,9 @@ if __name__ == '__main__':
                 env['RSL_RING'] = '0'
             elif part == 'ring':
                 env['RSL_RING'] = '1'
+            elif '=' in part:  # any other environment setting, e.g. RSL_DD_CP=42
+                k, val = part.split('=', 1)
+                env[k] = val
             else:
                 key, val = part[0], part[1:]
                 env[{'R': 'RSL_RING_R', 'L': 'RSL_RING_L', 'B': 'RSL_RING_BPC', 'F': 'F', 'O': 'RSL_RING_OWN', 'C': 'RSL_RING_CB', 'W': 'RSL_RING_WPE', 'Q': 'RSL_RING_Q', 'P': 'RSL_RING_PROF', 'T': 'RSL_RING_CT'}[key]] = val
