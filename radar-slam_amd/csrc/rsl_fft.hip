@@ -1127,12 +1127,13 @@ hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, 
 // queues are chosen by the XCD each workgroup actually runs on (HW_REG_XCC_ID), so producer and consumer of a slab
 // always share an L2 whatever the placement; the host enables the path only on an 8-XCC device.
 //
-// Measured (tools/ring_ab.py, 2000 cfg2 frames, outputs bit-identical to K1 + K2): 7.4-7.5 ms per launch at R 6, L 5
-// vs 6.7-6.9 ms for K1 + K2 in the same processes, so the path is opt-in (RSL_RING=1).  The hand-off itself is cheap
-// (waits ~5 % of workgroup time, RSL_RING_PROF) and keeping the slabs in L2 barely matters (own-address slabs, no
-// reuse: 7.9 ms); the launch is bound by its single register / LDS budget: the range role needs 157 VGPRs and 42 KiB
-// of LDS, which caps the Doppler role at 3 workgroups per CU where K2 alone runs 7 (a Doppler tile takes 7.4 us here;
-// two tiles per item with both loads in flight need 187 VGPRs: 9.5 ms).
+// Measured (tools/ring_ab.py, 2000 cfg2 frames, outputs bit-identical to K1 + K2): 7.3 ms per launch (4-chirp range
+// tiles, R 8, L 5) vs 6.6-6.9 ms for K1 + K2 in the same processes, so the path is opt-in (RSL_RING=1).  The hand-off
+// itself is cheap (waits ~5 % of workgroup time at 3 workgroups per CU, RSL_RING_PROF) and keeping the slabs in L2
+// barely matters (own-address slabs, no reuse: 7.9 ms); the launch is bound by its single register / LDS budget.
+// With 8-chirp range tiles the range role needs 42 KiB of LDS (and, before the thread index was laundered, 157
+// VGPRs), capping the Doppler role at 3 workgroups per CU where K2 alone runs 7 (7.4-8.3 ms); 4-chirp tiles fit 6 per
+// CU but then the ring slots are waited on (range-tile waits 11-14 % of workgroup time).
 // ---------------------------------------------------------------------------------------------
 constexpr int kRingSlots = 8;  // launches in flight (round-robin, as K1's queues)
 constexpr int kRingMaxR = 16;  // ring slabs per XCD (counter slots)
@@ -1216,6 +1217,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 
     if (tid == 0) claim = atomicAdd(head, 1u);
     const unsigned iend = min(total, (run + 1) * (unsigned)Q);
     for (unsigned it = run * (unsigned)Q; it < iend; ++it) {
+    // a laundered thread index: per-thread addresses are recomputed per item instead of held across the loop
+    int tidv = tid;
+    asm volatile("" : "+v"(tidv));
     // decode: role, slab k of this XCD, tile j
     bool prod_role;
     unsigned k, j;
@@ -1241,43 +1245,43 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 
       const float4* src4 = reinterpret_cast<const float4*>(cube + ((size_t)fa * Ct + c0 + j * CB) * S);
       float4 nx[PF];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) nx[q] = ld16<true>(src4 + tid + q * NT);
+      for (int q = 0; q < PF; ++q) nx[q] = ld16<true>(src4 + tidv + q * NT);
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
-        const int idx = tid + q * NT;
+        const int idx = tidv + q * NT;
         const int rr = idx / H, s2 = idx - rr * H;
         const float4 tb = tab4[s2];
         buf[rr * LDS_S + lp(2 * s2)] = cmul(make_float2(nx[q].x, nx[q].y), make_float2(tb.x, tb.y));
         buf[rr * LDS_S + lp(2 * s2 + 1)] = cmul(make_float2(nx[q].z, nx[q].w), make_float2(tb.z, tb.w));
       }
       __syncthreads();
-      fft_rows<S, CB, NT, LDS_S, true>(buf, tS, tid);
+      fft_rows<S, CB, NT, LDS_S, true>(buf, tS, tidv);
       if (dc) {
-        if (tid < CB) buf[tid * LDS_S] = make_float2(0.f, 0.f);
+        if (tidv < CB) buf[tidv * LDS_S] = make_float2(0.f, 0.f);
       }
       const unsigned long long tw0 = prof ? clock64() : 0;
-      if (tid == 0 && use > 0) ring_wait(&sy.cons[x][r][0], (unsigned)NC * use);  // the slot's previous slab is read
+      if (tidv == 0 && use > 0) ring_wait(&sy.cons[x][r][0], (unsigned)NC * use);  // the slot's previous slab is read
       __syncthreads();
       if (prof) w_p += clock64() - tw0;
       float4* dst4 = reinterpret_cast<float4*>(wslab + (size_t)j * CB * S);
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
-        const int idx = tid + q * NT;
+        const int idx = tidv + q * NT;
         const int rr = idx / H, s2 = idx - rr * H;
         const float2 lo = buf[rr * LDS_S + lp(2 * s2)], hi = buf[rr * LDS_S + lp(2 * s2 + 1)];
         dst4[idx] = make_float4(lo.x, lo.y, hi.x, hi.y);  // plain stores: the lines stay in this XCD's L2
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) atomicAdd(&sy.prod[x][r][0], 1u);
+      if (tidv == 0) atomicAdd(&sy.prod[x][r][0], 1u);
       if (prof) { t_p += clock64() - t0; ++n_p; }
     } else {
       // ---- Doppler item: CT tiles of KB range bins (+ halo) of slab fa (K2's body); the loads of all CT tiles are in
       // flight together (memory-level parallelism at the kernel's low occupancy) ----
-      if (tid == 0) ring_wait(&sy.prod[x][r][0], (unsigned)NP * (use + 1));
+      if (tidv == 0) ring_wait(&sy.prod[x][r][0], (unsigned)NP * (use + 1));
       __syncthreads();
       if (prof) w_c += clock64() - t0;
-      const int ri = tid % KB, cs = tid / KB;
+      const int ri = tidv % KB, cs = tidv / KB;
       float2 ld[CT][PI + PH];
 #pragma unroll
       for (int u = 0; u < CT; ++u) {
@@ -1290,7 +1294,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 
         if (kh >= S) kh -= S;
 #pragma unroll
         for (int h = 0; h < PH; ++h) {
-          const int e = tid + h * NT;
+          const int e = tidv + h * NT;
           if ((2 * C) % NT == 0 || e < 2 * C) {
             const int side = e / C, c = e - side * C;
             ld[u][PI + h] = ld8<true>(wslab + (unsigned)(c * S + (side ? kh : kl)));
@@ -1305,7 +1309,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 
         for (int q = 0; q < PI; ++q) row[lp(q * CS)] = ld[u][q];
 #pragma unroll
         for (int h = 0; h < PH; ++h) {
-          const int e = tid + h * NT;
+          const int e = tidv + h * NT;
           if ((2 * C) % NT == 0 || e < 2 * C) {
             const int side = e / C, c = e - side * C;
             buf[(side ? NR - 1 : 0) * LDC + lp(c)] = ld[u][PI + h];
@@ -1313,10 +1317,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 
         }
         if (u == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every tile's rows are in registers
         __syncthreads();
-        if (u == 0 && tid == 0) atomicAdd(&sy.cons[x][r][0], 1u);  // the slot may be refilled
-        fft_rows<C, NR, NT, LDC, false, true>(buf, tC, tid);
+        if (u == 0 && tidv == 0) atomicAdd(&sy.cons[x][r][0], 1u);  // the slot may be refilled
+        fft_rows<C, NR, NT, LDC, false, true>(buf, tC, tidv);
         dd_tile_compute_reg<C, KB, NT, 0, 10>(buf, reinterpret_cast<float*>(buf + NR * LDC), S, k0, (unsigned)fa, rds,
-                                              thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow);
+                                              thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow, tidv);
         __syncthreads();
       }
       if (prof) { t_c += clock64() - t0; ++n_c; }
@@ -1381,7 +1385,7 @@ static hipError_t launch_rds_ring_t(hipStream_t st, const float2* cube, int F, i
   constexpr int BUF = (CB * LDS_S > NR * LDC + KB * (CC / 64) * 2) ? CB * LDS_S : NR * LDC + KB * (CC / 64) * 2;
   const size_t lds = sizeof(float2) * (size_t)(LDS_S + CC + BUF);
   const long nfa = (long)F * A;
-  int R = 6, L = 5;  // fastest measured (tools/ring_ab.py)
+  int R = 8, L = 5;  // fastest measured (tools/ring_ab.py)
   if (const char* e = getenv("RSL_RING_R")) R = atoi(e);
   if (const char* e = getenv("RSL_RING_L")) L = atoi(e);
   // a Doppler tile may only wait for items dequeued before it (L >= 1), and a range tile only for the slot's previous
@@ -1422,10 +1426,14 @@ hipError_t launch_rds_ring(hipStream_t st, const float2* cube, int F, int A, int
   *supported = rds_ring_supported(C, S) && ring_device_ok();
   if (!*supported || F <= 0) return hipSuccess;
   const char* e = getenv("RSL_RING_CT");  // Doppler tiles per item (1 or 2; A/B)
+  const char* cb = getenv("RSL_RING_CB");  // chirps per range tile (4: 26 KiB of LDS, 6 workgroups per CU; or 8)
   if (e && atoi(e) == 2)
     return launch_rds_ring_t<8, 0, 2>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi,
                                       mask, row_count, pk_pow, pk_group);
-  return launch_rds_ring_t<8, 0, 1>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi, mask,
+  if (cb && atoi(cb) == 8)
+    return launch_rds_ring_t<8, 0, 1>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi,
+                                      mask, row_count, pk_pow, pk_group);
+  return launch_rds_ring_t<4, 0, 1>(st, cube, F, A, Ct, c0, table, twS, twC, dc, work, rds, thr_p, i_lo, i_hi, mask,
                                     row_count, pk_pow, pk_group);
 }
 

@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u tools/ring_ab.py two two+RSL_DD_PERSIST=1 two+RSL_DD_PERSIST=1+RSL_DD_PWPE=6 two two+RSL_DD_PERSIST=1 two+RSL_DD_PERSIST=1+RSL_DD_PWPE=6 > gpurun_out/r2k_k2p.log 2>&1
-RSL_DD_PERSIST=1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_chain.py tests/test_gpu_pipelined.py > gpurun_out/r2k_k2ptest.log 2>&1
+timeout -k 10 300 env RSL_RING_CB=4 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ring.py > gpurun_out/r2k_ringtest.log 2>&1
+timeout -k 10 700 python -u tools/ring_ab.py two ring+R6+L5+P1 ring+R6+L5+C4+P1 ring+R8+L7+C4+P1 ring+R4+L3+C4 ring+R8+L5+C4 ring+R6+L5+C4+B4 two > gpurun_out/r2k_ring7.log 2>&1
