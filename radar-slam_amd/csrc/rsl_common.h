@@ -210,6 +210,19 @@ struct Dft {
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (observed placement, speed only), so
 // logical tile L = (b % 8) * (n / 8) + b / 8 gives each XCD a contiguous run of tiles, dispatched back to back:
 // tiles sharing halo cache lines then meet in the same 4 MiB L2.  The n % 8 tail keeps the identity order.
+// Inclusive scan of an int over the 64 lanes of a wave in DPP: row_shr 1 / 2 / 4 / 8 (bound_ctrl: 0 past the row
+// start), then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3.  Six VALU ops, no LDS round trips
+// (the __shfl_up form is six ds_bpermute).  Every lane must be active.
+RSL_DEV int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
 RSL_DEV long xcd_tile(long b, long n) {
   const long n8 = n & ~7L;
   return b < n8 ? (b & 7) * (n8 >> 3) + (b >> 3) : b;

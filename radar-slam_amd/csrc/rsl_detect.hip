@@ -240,12 +240,7 @@ constexpr int kEmitU = 4;  // phase-2 items per lane per trip
 
 RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
+  const int x = wave_incl_scan(v);
   if (lane == 63) wsum[wave] = x;
   __syncthreads();
   int pre = 0;

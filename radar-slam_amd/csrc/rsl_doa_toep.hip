@@ -231,7 +231,7 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
 // column n), so each lane computes the Toeplitz column of its own cell once and swaps the other K half with
 // lane l ^ 32 (no redundant loads or autocorrelations), and the fused ESPRIT / phase work of a pass is spread
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
-template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0>
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : 1))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
@@ -405,7 +405,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         else if constexpr (DBG != 1) copy_tile(sv1, acc1);
       }
     };
-    {
+    if constexpr (SKEW && NTC > 0 && KB == 1 && DBG == 0) {
+      // Skewed schedule: the two column tiles' MFMA chains run half a tile apart, so each chain's epilogue (tile max,
+      // record test, record copy) issues while the other chain's MFMAs execute instead of waiting for them; the A
+      // operands of tile t + 1 are read from LDS during tile t's first epilogue.  Same products and record order.
+      const half8 x0h = __builtin_bit_cast(half8, b0h[0]), x0l = __builtin_bit_cast(half8, b0l[0]);
+      const half8 x1h = __builtin_bit_cast(half8, b1h[0]), x1l = __builtin_bit_cast(half8, b1l[0]);
+      half8 ah, al;
+      floatx16 acc0, acc1;
+      auto lda = [&](int t) {
+        ah = __builtin_bit_cast(half8, tt[(t * 2 + 0) * 64 + lane]);
+        al = __builtin_bit_cast(half8, tt[(t * 2 + 1) * 64 + lane]);
+      };
+      auto chain = [&](floatx16& acc, const half8& xh, const half8& xl) {
+        acc = floatx16{};
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc, 0, 0, 0);
+      };
+      auto rec = [&](int t, const floatx16& acc, float& best, int& bt, double (&sv)[8]) {
+        const float m = tile_max(acc);
+        if (t == 0) {
+          typedef double doublex8 __attribute__((ext_vector_type(8)));
+          const doublex8 d = __builtin_bit_cast(doublex8, acc);
+          best = m;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sv[k] = d[k];
+          return;
+        }
+        if (m > best) {
+          best = m;
+          bt = t;
+          copy_tile(sv, acc);
+        }
+      };
+      lda(0);
+      chain(acc0, x0h, x0l);
+      chain(acc1, x1h, x1l);
+#pragma unroll
+      for (int t = 0; t < NTC; ++t) {
+        if (t + 1 < NTC) lda(t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        rec(t, acc0, best0, bt0, sv0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < NTC) chain(acc0, x0h, x0l);
+        __builtin_amdgcn_sched_barrier(0);
+        rec(t, acc1, best1, bt1, sv1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < NTC) chain(acc1, x1h, x1l);
+      }
+    } else {
       const int ntl = NTC ? NTC : ntiles;  // NTC: compile-time tile count (fully unrolled loop)
 #pragma unroll
       for (int t = 0; t < ntl; ++t) {
@@ -462,7 +511,12 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS>;
   if constexpr (MA == 8) {  // the 0.5-degree grid (G = 361: 12 tiles of 32): unrolled tile loop
     const char* eu = getenv("RSL_DOA_UNROLL");
-    if (ntiles == 12 && (!eu || atoi(eu) != 0)) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12>;
+    // skewed column-tile chains (default; RSL_DOA_SKEW=0 for the plain order): tools/doa_var_ab.py, one call,
+    // 3.77-3.78 vs 3.83-3.87 ms per 2000 cfg2 frames, outputs bit-identical
+    const char* es = getenv("RSL_DOA_SKEW");
+    const bool skew = !es || atoi(es) != 0;
+    if (ntiles == 12 && (!eu || atoi(eu) != 0))
+      kern = skew ? k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true> : k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12>;
   }
   if constexpr (MUSIC && !GMAX && !EXTRAS && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing studies only)
     if (const char* e = getenv("RSL_DOA_DBG")) {

@@ -475,7 +475,16 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   unsigned long long bal[8];  // this wave's ballot word of each of its rows (wave-uniform)
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) {
-    float l = __shfl_up(vm[rr], 1), r = __shfl_down(vm[rr], 1);
+    // neighbour lanes by DPP wavefront shifts (wave_shr:1 / wave_shl:1, one VALU op each) instead of ds_bpermute
+    // round trips through the LDS unit; lanes 0 / 63 take their outside neighbour from the exchange words below
+    float l, r;
+    if constexpr ((CP & 64) != 0) {
+      l = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vm[rr]), 0x138, 0xF, 0xF, false));
+      r = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(vm[rr]), 0x130, 0xF, 0xF, false));
+    } else {
+      l = __shfl_up(vm[rr], 1);
+      r = __shfl_down(vm[rr], 1);
+    }
     if (lane == 0) l = ch > 0 ? ex[rr * 2 * NCH + 2 * (ch - 1) + 1] : vm[rr];
     if (lane == 63) r = ch + 1 < NCH ? ex[rr * 2 * NCH + 2 * (ch + 1)] : vm[rr];
     const float m = fmaxf(fmaxf(l, vm[rr]), r);
@@ -495,10 +504,14 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   const unsigned long long myw = lane < KB * NCH ? wb[lane] : 0ull;
   const int cw = __popcll(myw);
   int incl = cw;
+  if constexpr ((CP & 64) != 0) {
+    incl = wave_incl_scan(incl);
+  } else {
 #pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const int v = __shfl_up(incl, dd);
-    if (lane >= dd) incl += v;
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const int v = __shfl_up(incl, dd);
+      if (lane >= dd) incl += v;
+    }
   }
   const int excl = incl - cw;
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
@@ -545,7 +558,8 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-// CP (cache policy) bit 0: nt interior loads, bit 1: nt RDS stores, bit 2: nt halo loads
+// CP (cache policy) bit 0: nt interior loads, bit 1: nt RDS stores, bit 2: nt halo loads; register body: bit 3 LDS-staged
+// peak powers, bit 4 16-B RDS stores, bit 5 16-B interior loads, bit 6 DPP neighbour lanes and wave scan
 template <int C, int KB, int NT, bool PAD, int DBG = 0, int CP = 0>
 __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
@@ -805,7 +819,9 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   constexpr int NT = 256;
   // nt RDS stores (the product output, not re-read by this stage; tools/cp_ab.py: 1.68 vs 1.70 ms per 1000 frames);
   // peak powers staged in LDS and stored block-wide (tools/pkb.sh: 187.2-188.5 k vs 184.1-185.2 k frames/s)
-  auto kern = pad ? k_doppler_detect<C, KB, NT, true, 0, 10> : k_doppler_detect<C, KB, NT, false>;
+  // DPP neighbour lanes and wave scan in the register tile body (CP bit 6; RSL_DD_CP=10 for the ds_bpermute form):
+  // tools/ring_ab.py, one call, K2 3.52 vs 3.76 ms per 2000 cfg2 frames, outputs bit-identical
+  auto kern = pad ? k_doppler_detect<C, KB, NT, true, 0, 74> : k_doppler_detect<C, KB, NT, false>;
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (timing only: results are wrong)
     const int v = atoi(e);
     if (v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, 10>;
@@ -826,6 +842,8 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
       if (v == 10) kern = k_doppler_detect<C, KB, NT, true, 0, 10>;
       if (v == 26) kern = k_doppler_detect<C, KB, NT, true, 0, 26>;
       if (v == 42) kern = k_doppler_detect<C, KB, NT, true, 0, 42>;  // 10 + 16-B interior loads
+      if (v == 74) kern = k_doppler_detect<C, KB, NT, true, 0, 74>;  // 10 + DPP neighbour lanes
+      if (v == 106) kern = k_doppler_detect<C, KB, NT, true, 0, 106>;  // 10 + 16-B loads + DPP
     }
   }
   if constexpr ((NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16)) {

@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 env RSL_RING_CB=4 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ring.py > gpurun_out/r2k_ringtest.log 2>&1
-timeout -k 10 700 python -u tools/ring_ab.py two ring+R6+L5+P1 ring+R6+L5+C4+P1 ring+R8+L7+C4+P1 ring+R4+L3+C4 ring+R8+L5+C4 ring+R6+L5+C4+B4 two > gpurun_out/r2k_ring7.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r2l_gputest.log 2>&1
+timeout -k 10 600 python -u bench.py > gpurun_out/r2l_bench.log 2>&1
+timeout -k 10 600 python -u bench.py --no-cpu-baseline > gpurun_out/r2l_bench2.log 2>&1
