@@ -8,8 +8,8 @@ One step = one pass of the full per-frame chain (configs[2]: RDS + peak detectio
 ESPRIT + least-squares velocity + trajectory integration) over a batch of F synthetic frames already
 resident in HBM.  Frames shard across ranks (one process per GPU, weak scaling, no data-path collective);
 the only exchange is the trajectory reduction of the north star: each rank scans its block's poses on the
-device, the ranks all-gather 16-double block summaries and then the per-frame poses over RCCL/xGMI.  Rank 0
-prints one JSON line.
+device, the ranks all-gather 16-double block summaries over RCCL/xGMI and the per-frame poses are gathered to rank 0,
+which smooths them across block edges.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -158,7 +158,7 @@ def cpu_baseline(procs=16, frames=2, ridge=0.01):
 
 def run_spectrum(args, world, rank, local, dev):
     """configs[1]: 8ch x 128chirp x 512 cube, 1000 frames per step, range-Doppler FFT + peaks + the MUSIC spectrum
-    of every unique cell (f32, grid-major [361, cells]; the reference keeps spectrum f64[G] per target,
+    of every unique cell (f32, cell-blocked [cells / 32, 361, 32]; the reference keeps spectrum f64[G] per target,
     angle_estimation.py:299).  One chain, no pipelining; the spectrum store dominates (51 MB per frame)."""
     import torch
     import torch.distributed as dist
@@ -212,7 +212,7 @@ def run_spectrum(args, world, rank, local, dev):
         per = lambda k: kt[k][0] / max(kt[k][1], 1)
         sbytes = nc * G * 4 + nc * A * 8  # spectrum store + signature gather
         t = per('doa_scan') * 1e-3
-        line["roofline"] = {"bound": "hbm", "kernel": "k_doa_scan (spectrum)", "achieved": sbytes / t / 1e9,
+        line["roofline"] = {"bound": "hbm", "kernel": "k_doa_toep (spectrum, Toeplitz f16 MFMA)", "achieved": sbytes / t / 1e9,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sbytes / t / 1e9 / HBM_PEAK_GBS,
                             "traffic": None, "avg_launch_ms": per('doa_scan'), "algorithmic_bytes_per_launch": sbytes}
         fb = 2 * A * C * S * 8 * F

@@ -143,7 +143,8 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
  *     (ncell = the lists' capacity: an overflowed list is processed up to its capacity), else ncell.
  *     steer_tab = device copy of the rsl_steer_table_build output; steer_c128 = device fp64 [G][M][2]
  *     steering matrix (needed by MUSIC with RSL_DOA_TOEPLITZ for its exact fp64 near-degenerate re-scan).
- *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; ignored when out_spec is requested).
+ *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; with out_spec it applies to the RSL_DOA_SPEC_BLOCKED layout
+ *     without out_gmax, the other spectrum requests take the f32 scan).
  *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
  *     at the argmax (unit-norm s); out_spec f32 [n, G] (nullable; [G][ncell] with RSL_DOA_SPEC_GMAJOR,
  *     [ceil(ncell / 32)][G][32] with RSL_DOA_SPEC_BLOCKED) = MUSIC

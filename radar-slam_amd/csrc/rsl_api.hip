@@ -405,7 +405,9 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
   Scope sc(h, RSL_K_DOA_SCAN);
-  if (toep && !out_spec && rsl::toep_table_fits(G, A) && getenv("RSL_DOA_FULL") == nullptr) {
+  // the Toeplitz f16-MFMA scan: argmax only, or with the whole spectrum in the cell-blocked layout (no gmax there)
+  const bool toep_spec = out_spec && (method & RSL_DOA_SPEC_BLOCKED) && !out_gmax;
+  if (toep && (!out_spec || toep_spec) && rsl::toep_table_fits(G, A) && getenv("RSL_DOA_FULL") == nullptr) {
     int nt32 = (G + 31) / 32;
     nt32 += nt32 & 1;
     const float* tp = (const float*)steer_tab + steer_f32_floats(G, A);
@@ -413,7 +415,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
                      rsl::launch_doa_toep(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
                                           (const int*)c_rc, (const long long*)ncell_dev, ncell, tp, nt32, G, music,
                                           (const double*)steer_c128, (int*)out_idx, (float*)out_gmax, 0.0,
-                                          nullptr, nullptr),
+                                          nullptr, nullptr, toep_spec ? (float*)out_spec : nullptr),
                      "doa_toep");
   }
   long long blocks = 0;  // 0: all resident workgroups (occupancy x CUs)

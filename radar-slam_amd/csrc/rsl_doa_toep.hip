@@ -231,15 +231,18 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
 // column n), so each lane computes the Toeplitz column of its own cell once and swaps the other K half with
 // lane l ^ 32 (no redundant loads or autocorrelations), and the fused ESPRIT / phase work of a pass is spread
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
-template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false>
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false,
+          bool SPEC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : 1))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
                                                   const double* __restrict__ steer64, int* __restrict__ out_idx,
                                                   float* __restrict__ out_gmax, double esprit_scale,
-                                                  double* __restrict__ out_esprit, double* __restrict__ out_phase) {
+                                                  double* __restrict__ out_esprit, double* __restrict__ out_phase,
+                                                  float* __restrict__ out_spec) {
   extern __shared__ uint4 tt[];  // the whole Toeplitz operand table (<= 64 KiB)
+  __shared__ float sstg[SPEC ? 4 * 512 : 1];  // SPEC: per-wave store stage
   {
     const long long nc = list_count(ncell_dev, ncell_host);
     if ((long long)blockIdx.x * 256 >= nc) return;  // a block past the cells (capacity-sized grids): no table load
@@ -405,6 +408,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         else if constexpr (DBG != 1) copy_tile(sv1, acc1);
       }
     };
+    // SPEC: the whole spectrum of both column tiles, cell-blocked f32 [ceil(n / 32)][G][32] (RSL_DOA_SPEC_BLOCKED):
+    // MUSIC 1/(M - P) with the reference's den > 1e-12 rule (angle_estimation.py:149-152; a zero signature has
+    // den = M - 1: its eigenvectors are the identity) or the beamforming P (:227-251), P = acc / 2^8.  Lane (n, h)
+    // holds rows (i & 3) + 8 (i >> 2) + 4 h of column n, so each store instruction writes two 128-B runs.
+    bool zc0 = false, zc1 = false;  // zero signature of column tile 0 / 1's cell n
+    if constexpr (SPEC) {
+      const bool zown = !(ar[0] > 0.f);
+      const bool zoth = __shfl_xor((int)zown, 32) != 0;
+      zc0 = h ? zoth : zown;
+      zc1 = h ? zown : zoth;
+    }
+    // Stores go through a per-wave 2 KiB LDS stage, half a tile (16 grid points x 32 cells) at a time, so that each
+    // store instruction writes 1 KiB (8 whole 128-B lines, consecutive grid points) instead of two 128-B runs.
+    auto spec_tile = [&](int t, const floatx16& acc, int ct) {
+      if constexpr (SPEC) {
+        if (ch * 64 + 32 * ct >= ncell) return;  // a column tile past the cells (wave-uniform)
+        const bool zc = ct ? zc1 : zc0;
+        const float Mf = (float)A;
+        float* stw = sstg + wave * 512;
+        float* dst = out_spec + ((size_t)(2 * ch + ct) * G) * 32;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+          for (int ii = 0; ii < 8; ++ii) {
+            const int i = 8 * half + ii;
+            const int r = (i & 3) + 8 * ((i >> 2) & 1) + 4 * h;  // row within the half (0..15)
+            const float P = acc[i] * (1.f / kToepScale);
+            float v = P;
+            if constexpr (MUSIC) {
+              const float d = zc ? Mf - 1.f : Mf - P;
+              v = d > 1e-12f ? __builtin_amdgcn_rcpf(d) : 0.f;
+            }
+            stw[r * 32 + (lane & 31)] = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int r = (lane >> 3) + 8 * q;
+            const float4 v = reinterpret_cast<const float4*>(stw)[r * 8 + (lane & 7)];
+            const int g = 32 * t + 16 * half + r;
+            if (g < G) reinterpret_cast<float4*>(dst + (size_t)g * 32)[lane & 7] = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    };
     if constexpr (SKEW && NTC > 0 && KB == 1 && DBG == 0) {
       // Skewed schedule: the two column tiles' MFMA chains run half a tile apart, so each chain's epilogue (tile max,
       // record test, record copy) issues while the other chain's MFMAs execute instead of waiting for them; the A
@@ -447,10 +496,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         if (t + 1 < NTC) lda(t + 1);
         __builtin_amdgcn_sched_barrier(0);
         rec(t, acc0, best0, bt0, sv0);
+        spec_tile(t, acc0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NTC) chain(acc0, x0h, x0l);
         __builtin_amdgcn_sched_barrier(0);
         rec(t, acc1, best1, bt1, sv1);
+        spec_tile(t, acc1, 1);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NTC) chain(acc1, x1h, x1l);
       }
@@ -461,6 +512,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         floatx16 acc0, acc1;
         mma(t, acc0, acc1);
         record(t, acc0, acc1);
+        spec_tile(t, acc0, 0);
+        spec_tile(t, acc1, 1);
       }
     }
     int i0 = 15, i1 = 15;
@@ -503,22 +556,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
   }
 }
 
-template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS>
+template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, bool SPEC = false>
 static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                                 const int* c_rc, const long long* ncell_dev, long long ncell_host, const uint4* tab,
                                 int ntiles, int G, const double* steer64, int* out_idx, float* out_gmax,
-                                double esprit_scale, double* out_esprit, double* out_phase, int max_blocks) {
-  auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS>;
+                                double esprit_scale, double* out_esprit, double* out_phase, int max_blocks,
+                                float* out_spec = nullptr) {
+  auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 0, false, SPEC>;
   if constexpr (MA == 8) {  // the 0.5-degree grid (G = 361: 12 tiles of 32): unrolled tile loop
     const char* eu = getenv("RSL_DOA_UNROLL");
     // skewed column-tile chains (default; RSL_DOA_SKEW=0 for the plain order): tools/doa_var_ab.py, one call,
     // 3.77-3.78 vs 3.83-3.87 ms per 2000 cfg2 frames, outputs bit-identical
     const char* es = getenv("RSL_DOA_SKEW");
     const bool skew = !es || atoi(es) != 0;
-    if (ntiles == 12 && (!eu || atoi(eu) != 0))
+    if (ntiles == 12 && (!eu || atoi(eu) != 0) && !SPEC)  // the spectrum scan keeps the rolled tile loop
       kern = skew ? k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true> : k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12>;
   }
-  if constexpr (MUSIC && !GMAX && !EXTRAS && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing studies only)
+  if constexpr (MUSIC && !GMAX && !EXTRAS && !SPEC && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing only)
     if (const char* e = getenv("RSL_DOA_DBG")) {
       const int v = atoi(e);
       if (ntiles == 12) {  // the unrolled form the bench runs
@@ -549,14 +603,15 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   if (ppw > 0) blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
-                     ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase);
+                     ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,
+                     out_spec);
   return hipGetLastError();
 }
 
 hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
                            int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
-                           double esprit_scale, double* out_esprit, double* out_phase) {
+                           double esprit_scale, double* out_esprit, double* out_phase, float* out_spec) {
   if (A < 1 || A > 16 || (ntiles32 & 1)) return hipErrorInvalidValue;
   if (music && !steer64) return hipErrorInvalidValue;
   if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
@@ -574,6 +629,19 @@ hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int 
   }                                                                                                              \
   if (gm) return ex ? launch_toep_t<MA, KB, false, true, true>(ARGS) : launch_toep_t<MA, KB, false, true, false>(ARGS); \
   return ex ? launch_toep_t<MA, KB, false, false, true>(ARGS) : launch_toep_t<MA, KB, false, false, false>(ARGS);
+  if (out_spec) {  // the spectrum-writing scan (cell-blocked layout), no GMAX
+    if (gm) return hipErrorInvalidValue;
+#define GOS(MA, KB)                                                                                              \
+  if (music) return ex ? launch_toep_t<MA, KB, true, false, true, true>(ARGS, out_spec)                          \
+                       : launch_toep_t<MA, KB, true, false, false, true>(ARGS, out_spec);                        \
+  return ex ? launch_toep_t<MA, KB, false, false, true, true>(ARGS, out_spec)                                    \
+            : launch_toep_t<MA, KB, false, false, false, true>(ARGS, out_spec);
+    if (A <= 8) {
+      GOS(8, 1)
+    }
+    GOS(16, 2)
+#undef GOS
+  }
   if (A <= 8) {
     GO(8, 1)
   }

@@ -219,8 +219,8 @@ class Context:
             want_gmax: bool = False, want_spec: bool = False, out_idx=None, fast: bool = True,
             spec_gmajor: bool = False, spec_blocked: bool = False, out_spec=None):
         """Steering-scan argmax per cell.  fast=True (default) uses the Toeplitz f16-MFMA path when the
-        steering matrix is a uniform linear array and no spectrum is requested; fast=False forces the f32
-        [Re; Im] MFMA scan.  want_spec: the spectrum, f32 [n, G]; [G, n] (n = the capacity) with spec_gmajor;
+        steering matrix is a uniform linear array and either no spectrum or the cell-blocked spectrum (without
+        gmax) is requested; fast=False forces the f32 [Re; Im] MFMA scan.  want_spec: the spectrum, f32 [n, G]; [G, n] (n = the capacity) with spec_gmajor;
         [ceil(n / 32), G, 32] with spec_blocked (see spectrum_rows)."""
         torch = self.torch
         _, A, S, C = rds.shape
@@ -239,8 +239,8 @@ class Context:
             m |= _lib.DOA_SPEC_BLOCKED
         elif want_spec and spec_gmajor:
             m |= _lib.DOA_SPEC_GMAJOR
-        if fast and steer['toeplitz'] and not want_spec:
-            m |= _lib.DOA_TOEPLITZ
+        if fast and steer['toeplitz'] and (not want_spec or (spec_blocked and not want_gmax)):
+            m |= _lib.DOA_TOEPLITZ  # the f16-MFMA Toeplitz scan (argmax, or with the cell-blocked spectrum)
         self.check(self.lib.rsl_doa(self.h, _ptr(rds), A, S, C, _ptr(c_frame), _ptr(c_rc), _ptr(n_dev), cap,
                                     _ptr(steer['tab']), _ptr(steer['c128']), steer['G'], m, _ptr(idx), _ptr(gmax),
                                     _ptr(spec)), 'rsl_doa')

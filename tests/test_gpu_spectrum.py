@@ -1,6 +1,7 @@
 """Batched MUSIC / beamforming spectrum (configs[1]: "range-Doppler FFT + MUSIC spectrum"): RadarChain with
-spectrum=True writes f32 cell-blocked [cells / 32, G, 32] from the f32-MFMA steering scan (k_doa_scan,
-RSL_DOA_SPEC_BLOCKED).
+spectrum=True writes f32 cell-blocked [cells / 32, G, 32] (RSL_DOA_SPEC_BLOCKED) from the Toeplitz f16-MFMA scan
+(k_doa_toep with SPEC, uniform linear arrays); the f32-MFMA steering scan (k_doa_scan) writes every layout and is
+the general path.
 The reference stores spectrum f64[G] per target (angle_estimation.py:143-154, :299).
 
 Tolerance: MUSIC values are 1/den with den = M - |a^H s|^2 (rank-1 closed form); fp32 |a^H s|^2 from
@@ -76,12 +77,53 @@ def test_spectrum_layouts_agree(ctx):
     ch.run(ctx.to_dev(frames.astype(np.complex64)))
     nc = ch.totals()[1]
     L = ch.lists
-    _, _, s_cm = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True)
+    _, _, s_cm = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True, fast=False)
     _, _, s_gm = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
-                         spec_gmajor=True)
+                         spec_gmajor=True, fast=False)
     _, _, s_bl = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
-                         spec_blocked=True)
+                         spec_blocked=True, fast=False)
     from rsl.runtime import spectrum_rows
     torch.cuda.synchronize()
     assert torch.equal(s_cm, s_gm.t())
     assert torch.equal(s_cm, spectrum_rows(s_bl, nc))
+
+
+@pytest.mark.parametrize('method', ['music', 'beamforming'])
+def test_toeplitz_spectrum_matches_f32_scan(ctx, method):
+    """The Toeplitz spectrum (f16 hi/lo products) against the f32-MFMA scan's spectrum of the same cells: MUSIC den
+    within DEN_ATOL, beamforming |a^H s|^2 within 2e-5, same argmax wherever the f32 scan's top-2 gap is clear, and
+    the argmax is a maximum of the written spectrum."""
+    import rsl
+    import torch
+    from rsl.runtime import spectrum_rows
+    frames = _frames(8, 128, 51.2e-6, 2)
+    cfg = rsl.ChainConfig(num_antennas=8, num_chirps=128, chirp_duration=51.2e-6, method=method)
+    ch = rsl.RadarChain(cfg, 2, ctx)
+    ch.run(ctx.to_dev(frames.astype(np.complex64)), esprit=False, velocity=False)
+    nc = ch.totals()[1]
+    L = ch.lists
+    i_t, _, s_t = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
+                          spec_blocked=True)
+    i_f, _, s_f = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=nc, want_spec=True,
+                          spec_blocked=True, fast=False)
+    torch.cuda.synchronize()
+    st = spectrum_rows(s_t, nc).cpu().numpy().astype(np.float64)
+    sf = spectrum_rows(s_f, nc).cpu().numpy().astype(np.float64)
+    it, jf = i_t[:nc].cpu().numpy(), i_f[:nc].cpu().numpy()
+    n = np.arange(nc)
+    assert (st[n, it] == st.max(axis=1)).all()
+    if method == 'music':
+        assert ((st > 0) == (sf > 0)).all()
+        dt = np.where(st > 0, 1.0 / np.where(st > 0, st, 1.0), 0.0)
+        df = np.where(sf > 0, 1.0 / np.where(sf > 0, sf, 1.0), 0.0)
+        err = np.abs(dt - df).max()
+        key = 8.0 - df
+    else:
+        err = np.abs(st - sf).max()
+        key = sf
+    srt = np.sort(key, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-5 * np.abs(srt[:, -1])
+    print(f'{method}: {nc} cells, max diff {err:.2e}, argmax differs at {(it != jf).sum()} cells '
+          f'({(it != jf)[clear].sum()} with a clear gap)')
+    assert err < DEN_ATOL
+    assert (it == jf)[clear].all()
