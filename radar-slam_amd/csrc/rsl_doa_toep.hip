@@ -274,10 +274,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
       if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
     }
   }
+  // The argmax (and gmax) of a pass is stored at the start of the NEXT pass, after the wait for that pass's prefetched
+  // signatures: stored at the end of its own pass it sat in front of that wait (stores count in vmcnt, and a store
+  // under a branch makes the compiler wait for vmcnt(0)), so every pass waited out a store round trip.
+  int pc = -1;  // pending store: cell (-1: none; cell counts < 2^31, checked by the launcher), grid index, gmax
+  int pidx = 0;
+  float pgv = 0.f;
   for (; ch < nch; ch += stride) {
     float2 s[MA];
 #pragma unroll
     for (int m = 0; m < MA; ++m) s[m] = ns[m];
+    if (pc >= 0) {
+      out_idx[pc] = pidx;
+      if constexpr (GMAX) out_gmax[pc] = pgv;
+    }
     const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
     if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
@@ -549,10 +559,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         exact_scan<MA>(sr, A, G, steer64, bidx, gval);
       }
     }
-    if (c < ncell) {
-      out_idx[c] = bidx;
-      if constexpr (GMAX) out_gmax[c] = gval;
-    }
+    pc = c < ncell ? (int)c : -1;
+    pidx = bidx;
+    pgv = gval;
+  }
+  if (pc >= 0) {
+    out_idx[pc] = pidx;
+    if constexpr (GMAX) out_gmax[pc] = pgv;
   }
 }
 
@@ -612,7 +625,7 @@ hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int 
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
                            int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
                            double esprit_scale, double* out_esprit, double* out_phase, float* out_spec) {
-  if (A < 1 || A > 16 || (ntiles32 & 1)) return hipErrorInvalidValue;
+  if (A < 1 || A > 16 || (ntiles32 & 1) || ncell_host >= (1LL << 31) - 64) return hipErrorInvalidValue;
   if (music && !steer64) return hipErrorInvalidValue;
   if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
   const long long max_blocks = ncell_dev ? 0 : (ncell_host + 255) / 256;  // 4 waves x 64 cells
