@@ -1,3 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u tools/doa_var_ab.py DOA_ARGMAX=1 DOA_ARGMAX=1+RSL_DOA_SKEW=0 DOA_ARGMAX=1 DOA_ARGMAX=1+RSL_DOA_SKEW=0 > gpurun_out/r2l_doa4.log 2>&1
+timeout -k 10 800 bash tools/chain_counters.sh > gpurun_out/r2l_chainctr.log 2>&1
