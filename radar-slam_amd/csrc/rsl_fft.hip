@@ -843,6 +843,8 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
       if (v == 26) kern = k_doppler_detect<C, KB, NT, true, 0, 26>;
       if (v == 42) kern = k_doppler_detect<C, KB, NT, true, 0, 42>;  // 10 + 16-B interior loads
       if (v == 74) kern = k_doppler_detect<C, KB, NT, true, 0, 74>;  // 10 + DPP neighbour lanes
+      // measured with the DPP body (tools/ring_ab.py, one call): nt interior loads 3.58-3.59, nt interior + halo
+      // loads 3.92, 16-B RDS stores 3.59 vs 3.55-3.56 ms per 2000 frames
       if (v == 106) kern = k_doppler_detect<C, KB, NT, true, 0, 106>;  // 10 + 16-B loads + DPP
     }
   }
