@@ -156,6 +156,21 @@ def cpu_baseline(procs=16, frames=2, ridge=0.01):
                                       f"MUSIC / ESPRIT over all peaks, LS velocity); {t_vec:.1f} s wall"})
 
 
+SPEC_PROFILE = os.path.join(ROOT, 'profiles', 'r2b_spectrum_pmc.json')  # tools/profile_spectrum.sh
+
+
+def spectrum_traffic(frames):
+    """HBM bytes per launch of the spectrum scan (k_doa_toep with SPEC) from the committed configs[1] PMC profile."""
+    try:
+        prof = json.load(open(SPEC_PROFILE))
+    except (OSError, ValueError):
+        return None
+    for name, e in prof.get('kernels', {}).items():
+        if name.startswith('rsl::k_doa_toep') and 'hbm_bytes' in e:
+            return e['hbm_bytes'] * frames / prof.get('frames_per_launch', 1000)
+    return None
+
+
 def run_spectrum(args, world, rank, local, dev):
     """configs[1]: 8ch x 128chirp x 512 cube, 1000 frames per step, range-Doppler FFT + peaks + the MUSIC spectrum
     of every unique cell (f32, cell-blocked [cells / 32, 361, 32]; the reference keeps spectrum f64[G] per target,
@@ -214,7 +229,8 @@ def run_spectrum(args, world, rank, local, dev):
         t = per('doa_scan') * 1e-3
         line["roofline"] = {"bound": "hbm", "kernel": "k_doa_toep (spectrum, Toeplitz f16 MFMA)", "achieved": sbytes / t / 1e9,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sbytes / t / 1e9 / HBM_PEAK_GBS,
-                            "traffic": None, "avg_launch_ms": per('doa_scan'), "algorithmic_bytes_per_launch": sbytes}
+                            "traffic": spectrum_traffic(F), "avg_launch_ms": per('doa_scan'),
+                            "algorithmic_bytes_per_launch": sbytes}
         fb = 2 * A * C * S * 8 * F
         tf = (per('range_fft') + per('doppler_fft')) * 1e-3
         line["fft_stage"] = {"bound": "hbm", "achieved": fb / tf / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
