@@ -1,3 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 700 python -u tools/ring_ab.py two two+RSL_DD_CP=75 two+RSL_DD_CP=79 two+RSL_DD_CP=90 two two+RSL_DD_CP=75 two+RSL_DD_CP=79 two+RSL_DD_CP=90 > gpurun_out/r2l_k2cp.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_spectrum.py -s > gpurun_out/r2m_spectest.log 2>&1
