@@ -17,6 +17,7 @@ MODULES = {
     'src.algorithms.velocity_solver_improved': 'src/algorithms/velocity_solver_improved.py',
     'src.algorithms.advanced_velocity_optimization': 'src/algorithms/advanced_velocity_optimization.py',
     'evaluation.compute_pose_error': 'evaluation/compute_pose_error.py',
+    'evaluation.compute_velocity_error': 'evaluation/compute_velocity_error.py',
 }
 
 
