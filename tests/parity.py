@@ -58,12 +58,13 @@ def peak_diff(gpu_mask, ref_rds, *, threshold_db=-20.0, gate=(0, 1 << 30)):
     return int(gpu_mask.sum()), int(ref_mask.sum()), int(diff.sum()), int(unexpl.sum())
 
 
-def doa_flip_budget(n_cells, num_antennas=8):
+def doa_flip_budget(n_cells, num_antennas=8, search_resolution=0.5):
     """Largest accepted number of explained flips among n_cells cells: DOA_FLIP_FRAC per cell for an 8-element
-    array, scaled by 8 / M for smaller arrays (the beam, and with it the band of grid points whose power lies within
-    fp32 rounding of the maximum, widens as 1 / M).  Measured on MI355X (r2): cfg2 4 / 60000 (6.7e-5), a4 (M = 4)
+    array on the reference's 0.5-degree grid, scaled by 8 / M for smaller arrays (the beam, and with it the band of
+    grid points whose power lies within fp32 rounding of the maximum, widens as 1 / M) and by 0.5 / resolution for
+    finer grids (more grid points in that band; tests/test_gpu_sweep.py measured 5 / 15692 at 0.25 degrees).  Measured on MI355X (r2): cfg2 4 / 60000 (6.7e-5), a4 (M = 4)
     3 / 10502 (2.9e-4), cfg5 1 / 30000; every flip's reference relative gap <= 8.7e-8."""
-    return max(3, int(DOA_FLIP_FRAC * n_cells * max(1.0, 8.0 / num_antennas)))
+    return max(3, int(DOA_FLIP_FRAC * n_cells * max(1.0, 8.0 / num_antennas) * max(1.0, 0.5 / search_resolution)))
 
 
 def doa_diff(gpu_idx, ref_sigs, steer, method='music', stats=None):
