@@ -171,6 +171,30 @@ def spectrum_traffic(frames):
     return None
 
 
+def cu_masked_stream(dev, ncu, side, total=256):
+    """A HIP stream restricted to ncu of the device's CUs (hipExtStreamCreateWithCUMask), wrapped for torch.  The
+    CUs are taken in groups of 8 consecutive mask bits spread evenly over the mask (side 0 from the low groups' end of
+    each spread, side 1 from the other), so that both sides keep CUs on every XCD."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL('libamdhip64.so')
+    ng = total // 8
+    take = max(1, min(ng, round(ncu / 8)))
+    groups = [g for g in range(ng) if (g * take) // ng != ((g + 1) * take) // ng]
+    if side:
+        groups = [ng - 1 - g for g in groups]
+    words = [0] * (total // 32)
+    for g in groups:
+        for b in range(8 * g, 8 * g + 8):
+            words[b // 32] |= 1 << (b % 32)
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    st = ctypes.c_void_p()
+    torch.cuda.set_device(dev)
+    if hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(len(words)), arr) != 0:
+        raise RuntimeError('hipExtStreamCreateWithCUMask failed')
+    return torch.cuda.ExternalStream(st.value, device=dev)
+
+
 def run_spectrum(args, world, rank, local, dev):
     """configs[1]: 8ch x 128chirp x 512 cube, 1000 frames per step, range-Doppler FFT + peaks + the MUSIC spectrum
     of every unique cell (f32, cell-blocked [cells / 32, 361, 32]; the reference keeps spectrum f64[G] per target,
@@ -314,6 +338,10 @@ def main():
         chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
         chain = chains[0]
         sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        cum = os.environ.get('RSL_BENCH_CUMASK')  # "front:back" CU counts: the two halves on CU-masked streams
+        if cum:
+            nf, nbk = (int(x) for x in cum.split(':'))
+            sA, sB = cu_masked_stream(dev, nf, 0), cu_masked_stream(dev, nbk, 1)
         evA = [torch.cuda.Event() for _ in range(2)]
         evB = [torch.cuda.Event() for _ in range(2)]
         used = [False, False]
