@@ -123,6 +123,33 @@ RSL_DEV void split8(const float* v, uint4& hi, uint4& lo) {
   lo = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// The same hi/lo split straight from the unscaled autocorrelation, two entries per packed dword pair: entry x of the
+// Toeplitz column is v_x * g_x (v = r0-flag, Re r1, Im r1, ...; g = 1 for the first, inv for the others, 0 past
+// 2 MA - 1), and v_fma_mix{lo,hi}_f16 write the halves in place (hi = f16(v g), lo = f16(v g - hi), both halves of
+// a dword by one instruction each, no shift / or packing).  Values equal to toep_entries + split8.
+template <int MA, int KB>
+RSL_DEV void toep_split(const float (&ar)[MA], const float (&ai)[MA], float inv, uint4 (&hi)[2 * KB],
+                        uint4 (&lo)[2 * KB]) {
+  auto val = [&](int x) { return x == 0 ? (ar[0] > 0.f ? kToepScale : 0.f) : x < 2 * MA - 1 ? ((x & 1) ? ar[(x + 1) >> 1] : ai[x >> 1]) : 0.f; };
+  auto scl = [&](int x) { return x == 0 ? 1.f : x < 2 * MA - 1 ? inv : 0.f; };
+#pragma unroll
+  for (int q = 0; q < 2 * KB; ++q) {
+    unsigned h[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int x = 8 * q + 2 * j;
+      asm("v_fma_mixlo_f16 %0, %2, %3, 0\n\t"
+          "v_fma_mixhi_f16 %0, %4, %5, 0\n\t"
+          "v_fma_mixlo_f16 %1, %2, %3, -%0 op_sel_hi:[0,0,1]\n\t"
+          "v_fma_mixhi_f16 %1, %4, %5, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+          : "=&v"(h[j]), "=&v"(l[j])
+          : "v"(val(x)), "v"(scl(x)), "v"(val(x + 1)), "v"(scl(x + 1)));
+    }
+    hi[q] = make_uint4(h[0], h[1], h[2], h[3]);
+    lo[q] = make_uint4(l[0], l[1], l[2], l[3]);
+  }
+}
+
 // v_permlane32_swap on each dword: the upper 32 lanes of a are exchanged with the lower 32 lanes of b.
 RSL_DEV void swap32_u4(uint4& a, uint4& b) {
   unsigned av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
@@ -332,21 +359,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     // B operands of the two column tiles: own K half from the own cell, the other half from lane ^ 32
     uint4 b0h[KB], b0l[KB], b1h[KB], b1l[KB];
     {
-      float e[16 * KB];
+      uint4 eh[2 * KB], el[2 * KB];
       if constexpr (DBG == 4) {
+        float e[16 * KB];
 #pragma unroll
         for (int x = 0; x < 16 * KB; ++x) e[x] = s[x % MA].x;
+#pragma unroll
+        for (int q = 0; q < 2 * KB; ++q) split8(e + 8 * q, eh[q], el[q]);
       } else {
-        toep_entries<MA, KB>(ar, ai, inv, e);
+        toep_split<MA, KB>(ar, ai, inv, eh, el);
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         // E0 / E1 = the own cell's K rows 16 kb .. +7 / +8 .. +15.  Column tile 0 (cells of lanes 0-31) needs
         // [E0 of lanes 0-31 | E1 of lanes 0-31 moved up], column tile 1 [E0 of lanes 32-63 moved down | E1 of lanes
         // 32-63]: exactly what v_permlane32_swap does to the pair (E0, E1), one instruction per dword
-        uint4 h0h, h0l, h1h, h1l;
-        split8(e + 16 * kb, h0h, h0l);
-        split8(e + 16 * kb + 8, h1h, h1l);
+        uint4 h0h = eh[2 * kb], h0l = el[2 * kb], h1h = eh[2 * kb + 1], h1l = el[2 * kb + 1];
         swap32_u4(h0h, h1h);
         swap32_u4(h0l, h1l);
         b0h[kb] = h0h;
