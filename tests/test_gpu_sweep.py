@@ -2,8 +2,8 @@
 
 test_gpu_chain.py checks fixed shapes on the reference's own test scene (tests/test_synth_raw.py:165-190).  Here each
 case draws its own scene (3-12 scatterers: range, azimuth, RCS, radial velocity), noise power, frame shape, detection
-threshold, range gate, grid resolution, DoA method (MUSIC / beamforming, angle_estimation.py:109-154 / :227-251) and
-ridge, from a fixed seed, and checks RDS, peak masks and entry order, DoA argmax (the same relative-gap rule and flip
+threshold, range gate, window (hann / hamming / blackman, dechirp.py:99-106), DC removal, grid resolution, DoA method
+(MUSIC / beamforming, angle_estimation.py:109-154 / :227-251) and ridge, from a fixed seed, and checks RDS, peak masks and entry order, DoA argmax (the same relative-gap rule and flip
 budget as test_gpu_chain), ESPRIT, spatial phase and the velocity solve on 2 frames.
 """
 import numpy as np
@@ -27,7 +27,8 @@ def _case(k):
              for _ in range(rs.randint(3, 13))]
     kw = dict(threshold_db=float(rs.choice([-30.0, -20.0, -12.0])), min_range=float(rs.choice([0.0, 1.0, 5.0])),
               max_range=float(rs.choice([50.0, 200.0])), search_resolution=float(rs.choice([0.5, 1.0, 0.25])),
-              method=str(rs.choice(['music', 'beamforming'])), ridge=float(rs.choice([0.0, 0.01])))
+              method=str(rs.choice(['music', 'beamforming'])), ridge=float(rs.choice([0.0, 0.01])),
+              window_type=str(rs.choice(['hann', 'hamming', 'blackman'])), dc_removal=bool(rs.rand() < 0.75))
     return A, C, Tc, scene, float(10 ** rs.uniform(-3, -1)), kw
 
 
@@ -59,7 +60,8 @@ def test_random_scene_parity(ctx, k):
     tot_m = tot_n = 0
     stats = {}
     for f in range(F):
-        ref = O.range_doppler_spectrum(frames[f], chirp_duration=Tc)
+        ref = O.range_doppler_spectrum(frames[f], chirp_duration=Tc, window_type=cfg.window_type,
+                                       dc_removal=cfg.dc_removal)
         assert P.rds_error(rds[f], ref) <= P.RDS_ATOL_REL, (k, f)
         ng, nr, nd, nu = P.peak_diff(_mask_bool(words[f], C), ref, threshold_db=cfg.threshold_db,
                                      gate=(ch.i_lo, ch.i_hi))
