@@ -3,8 +3,10 @@
 test_gpu_chain.py checks fixed shapes on the reference's own test scene (tests/test_synth_raw.py:165-190).  Here each
 case draws its own scene (3-12 scatterers: range, azimuth, RCS, radial velocity), noise power, frame shape, detection
 threshold, range gate, window (hann / hamming / blackman, dechirp.py:99-106), DC removal, grid resolution, DoA method
-(MUSIC / beamforming, angle_estimation.py:109-154 / :227-251) and ridge, from a fixed seed, and checks RDS, peak masks and entry order, DoA argmax (the same relative-gap rule and flip
-budget as test_gpu_chain), ESPRIT, spatial phase and the velocity solve on 2 frames.
+(MUSIC / beamforming, angle_estimation.py:109-154 / :227-251) and ridge, from a fixed seed, and checks RDS, peak
+masks and entry order, DoA argmax (the same relative-gap rule and flip budget as test_gpu_chain), ESPRIT, spatial
+phase and the velocity solve on 2 frames; every third case also writes the spectrum of every cell (MUSIC 1/den or
+beamforming P, angle_estimation.py:143-154, :299) and checks it against the oracle's fp64 spectrum.
 """
 import numpy as np
 import pytest
@@ -48,11 +50,15 @@ def test_random_scene_parity(ctx, k):
         np.random.seed(7000 + 31 * k + f)
         frames.append(O.synthesize_frame(scene, chirp_duration=Tc, num_chirps=C, num_antennas=A, noise_power=noise))
     frames = np.stack(frames)
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, **kw)
+    spectrum = k % 3 == 0  # every third case also writes the spectrum of every cell (K5'', angle_estimation.py:299)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, spectrum=spectrum, **kw)
     ch = rsl.RadarChain(cfg, F, ctx)
     ch.run(ctx.to_dev(frames.astype(np.complex64)))
     r = ch.results()
     rds, words = ch.rds.cpu().numpy(), ch.mask.cpu().numpy()
+    if spectrum:
+        from rsl.runtime import spectrum_rows
+        spec = spectrum_rows(ch.spec, int(r['cell_base'][F])).cpu().numpy()
     grid_deg = O.azimuth_grid(cfg.search_range, cfg.search_resolution)
     steer = O.steering_matrix(grid_deg, A)
     lam = 3e8 / cfg.fc
@@ -84,6 +90,19 @@ def test_random_scene_parity(ctx, k):
         assert nun == 0, (k, f, nm, nun, stats)
         tot_m += nm
         tot_n += len(rc)
+        if spectrum:  # den = 1/spectrum against the oracle's fp64 M - |a^H s|^2 (MUSIC), P itself (beamforming)
+            got = spec[cs]
+            n = np.arange(len(rc))
+            assert (got[n, r['gidx'][cs]] == got.max(axis=1)).all(), k
+            if cfg.method == 'music':
+                want = O.music_spectrum_closed(sigs, steer)
+                assert ((got > 0) == (want > 0)).all(), k
+                dg = np.where(got > 0, 1.0 / np.where(got > 0, got, 1.0), 0.0)
+                dw = np.where(want > 0, 1.0 / np.where(want > 0, want, 1.0), 0.0)
+                err = np.abs(dg - dw).max()
+            else:
+                err = np.abs(got - O.beamforming_spectrum(sigs, steer)).max()
+            assert err < 2e-5, (k, f, err)
         if A >= 2:
             emax, nnan = P.esprit_diff(r['esprit'][cs], O.esprit_closed(sigs))
             assert nnan == 0 and emax <= P.ESPRIT_TOL_DEG, (k, f, emax, nnan)
