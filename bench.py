@@ -29,6 +29,7 @@ METRIC = "radar frames/sec end-to-end, 8ch×128chirp×512 cube; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
+DIST = False  # a torch.distributed process group is up (set in main)
 PROFILE = os.path.join(ROOT, 'profiles', 'r2n_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
@@ -220,17 +221,17 @@ def run_spectrum(args, world, rank, local, dev):
     if not args.no_timing:
         ctx.timing(True)
         ctx.timing_reset()
-    if world > 1:
+    if DIST:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if DIST:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if DIST:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -296,9 +297,13 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    global DIST
+    # RSL_BENCH_DIST=1: bring the process group up at world size 1 too (torchrun --nproc-per-node 1), so a one-GPU box
+    # runs the RCCL initialisation, barriers, the max-over-ranks all-reduce and the trajectory collectives
+    DIST = world > 1 or os.environ.get('RSL_BENCH_DIST') == '1'
     if 'RSL_BENCH_DEVICE' in os.environ:  # rehearsal of the N > 1 path on a one-GPU box (all ranks on one device)
         local = int(os.environ['RSL_BENCH_DEVICE'])
-    if world > 1:
+    if DIST:
         torch.cuda.set_device(local)
         backend = os.environ.get('RSL_BENCH_BACKEND', 'nccl')  # nccl = RCCL over xGMI; gloo only for rehearsals
         if backend == 'nccl':
@@ -344,6 +349,10 @@ def main():
             sA, sB = cu_masked_stream(dev, nf, 0), cu_masked_stream(dev, nbk, 1)
         evA = [torch.cuda.Event() for _ in range(2)]
         evB = [torch.cuda.Event() for _ in range(2)]
+        # the trajectory (scan, RCCL summary all-gather, pose gather to rank 0, smoothing) on a third stream, so the
+        # collectives' latency stays off the back stream: batch i + 1's DoA does not wait for batch i's gather
+        sC = torch.cuda.Stream(dev) if os.environ.get('RSL_BENCH_TRAJ_STREAM', '1') != '0' else None
+        evC = [torch.cuda.Event() for _ in range(2)]
         used = [False, False]
 
     # 0: offsets + compaction on the front stream; 1: compaction on the back stream; 2: both on the back stream
@@ -360,9 +369,17 @@ def main():
             evA[k].record(sA)
         with torch.cuda.stream(sB):
             sB.wait_event(evA[k])
+            if sC is not None and used[k]:
+                sB.wait_event(evC[k])  # batch i-2's trajectory step has read chain k's velocities
             ch.run_back(emit=EMIT_BACK > 0, offsets=EMIT_BACK == 2)
-            reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
+            if sC is None:
+                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
             evB[k].record(sB)
+        if sC is not None:
+            with torch.cuda.stream(sC):
+                sC.wait_event(evB[k])
+                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
+                evC[k].record(sC)
         used[k] = True
 
     def step(i):
@@ -387,18 +404,18 @@ def main():
     if not args.no_timing:
         ctx.timing(True)
         ctx.timing_reset()
-    if world > 1:
+    if DIST:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if DIST:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if DIST:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -418,7 +435,7 @@ def main():
     fps = frames_total / elapsed
 
     if rank != 0:
-        if world > 1:
+        if DIST:
             dist.destroy_process_group()
         return
     G = len(chain.grid)
@@ -504,7 +521,7 @@ def main():
         except Exception as e:  # the baseline is reported, never the target
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if DIST:
         dist.destroy_process_group()
 
 

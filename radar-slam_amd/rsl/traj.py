@@ -137,13 +137,15 @@ class TrajectoryReducer:
         self.group = group
         import torch.distributed as dist
         self.dist = dist
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
-        self.gloo = self.world > 1 and dist.get_backend(group) == 'gloo'  # gloo gathers host tensors only
+        # collectives whenever a process group is up (also at world size 1: one rank still runs the RCCL calls)
+        self.on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.on else 1
+        self.rank = dist.get_rank(group) if self.on else 0
+        self.gloo = self.on and dist.get_backend(group) == 'gloo'  # gloo gathers host tensors only
         self.summaries = e((self.world, SUMMARY), torch.float64)
         self.poses = e((self.F, 7), torch.float64)
         self.root = self.rank == 0
-        self.all_poses = (e((self.world * self.F, 7), torch.float64) if self.world > 1 else self.poses) \
+        self.all_poses = (e((self.world * self.F, 7), torch.float64) if self.on else self.poses) \
             if self.root else None
         self.smoother = StreamingSmoother(smoothing_window, lambda x: smooth(ctx, x, smoothing_window), torch.cat) \
             if (smoothing and self.root) else None
@@ -161,7 +163,7 @@ class TrajectoryReducer:
         c.check(c.lib.rsl_traj_scan(c.h, _ptr(vel), int(vstride), int(nv), _ptr(omega), int(ostride), None,
                                     self.dt, self.F, self.method, _ptr(self.pos), _ptr(self.quat),
                                     _ptr(self.summary)), 'rsl_traj_scan')
-        if self.world > 1:
+        if self.on:
             if self.gloo:
                 hs = torch.empty((self.world, SUMMARY), dtype=torch.float64)
                 self.dist.all_gather_into_tensor(hs.view(-1), self.summary.cpu(), group=self.group)
@@ -176,7 +178,7 @@ class TrajectoryReducer:
         c.check(c.lib.rsl_traj_apply(c.h, _ptr(self.pos), _ptr(self.quat), self.F, _ptr(self.base)), 'rsl_traj_apply')
         self.poses[:, 0:3].copy_(self.pos)
         self.poses[:, 3:7].copy_(self.quat)
-        if self.world > 1:
+        if self.on:
             self._gather()
         if not self.root:
             return None
