@@ -260,7 +260,7 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false,
           bool SPEC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : 1))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : (SPEC ? 1 : 3)))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
