@@ -16,7 +16,8 @@ __device__ __forceinline__ long long list_count(const long long* dev, long long 
 // K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
 // cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
-                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported);
+                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
+                            signed char* wexp = nullptr);
 // K2: Doppler FFT (C points) + fftshift on both axes, transposed store.
 // work c64 [F, A, C, S] -> rds c64 [F, A, S, C]
 hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
@@ -28,7 +29,11 @@ bool doppler_detect_supported(int C, int S);
 float threshold_as_float(double thr);  // largest float t <= thr
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group);
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group,
+                                 const signed char* wexp = nullptr);
+// wexp non-null (both launches): `work` holds packed rows (24-bit mantissas, int8 exponents at wexp; rsl_fft.hip
+// pk_pack) instead of c64 -- only where work_pack_ok(C, S).
+bool work_pack_ok(int C, int S);
 // K12 + K3' (rsl_rds_fused.hip): one-pass range + Doppler FFT per (slab, range class) with the Doppler-direction half
 // of detection (Doppler 3-max + candidate bits into `work`), then the range-direction finish -> the same mask /
 // row_count / tile-compact peak powers as launch_doppler_detect.  S = 512, C = 128; opt-in with RSL_FUSED=1 (slower).

@@ -59,7 +59,8 @@ def cubes(ctx):
     (48, {'RSL_RING_BPC': '1'}),                        # one workgroup per CU
 ])
 def test_ring_matches_two_kernel_path(ctx, cubes, F, env):
-    ref = _run(ctx, cubes[F], F, {'RSL_RING': '0'})
+    # the two-kernel reference with c64 `work` rows (the ring hands over unpacked range spectra)
+    ref = _run(ctx, cubes[F], F, {'RSL_RING': '0', 'RSL_WORK_PACK': '0'})
     got = _run(ctx, cubes[F], F, dict(env, RSL_RING='1'))
     assert ctx.lib.rsl_ring_faults(ctx.h) == 0
     assert got['grp'] == ref['grp']

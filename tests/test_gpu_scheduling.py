@@ -37,6 +37,13 @@ def _run(ctx, ch, cube, dyn):
     return [t.clone() for t in (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow)]
 
 
+def _bits(t):
+    # bitwise: packed `work` rows (24-bit mantissas) reinterpreted as c64 include NaN patterns
+    if t.is_complex():
+        t = t.view(torch.float32)
+    return t.view(torch.int32) if t.dtype == torch.float32 else t
+
+
 @pytest.mark.parametrize('name', list(SHAPES))
 def test_dequeue_matches_static_walk(ctx, name):
     import rsl
@@ -51,4 +58,4 @@ def test_dequeue_matches_static_walk(ctx, name):
     for rep in range(21):
         got = _run(ctx, ch, cube, '1')
         for a, b, what in zip(ref, got, ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
-            assert torch.equal(a, b), f'{name}: {what} differs on launch {rep}'
+            assert torch.equal(_bits(a), _bits(b)), f'{name}: {what} differs on launch {rep}'
