@@ -16,12 +16,15 @@ SHAPES = {  # name: (F, A, C, T_c)  -> K1 tiles = F * A * ceil(C / 8) at S = 512
     'ragged': (3, 3, 24, 51.2e-6),       # 27 tiles over 8 XCDs (3 or 4 each)
     'cfg1': (5, 8, 64, 25.6e-6),         # S = 256
     'cfg2': (40, 8, 128, 51.2e-6),       # 5120 tiles: 6.7 per resident workgroup
+    'cfg2_pack': (40, 8, 128, 51.2e-6),  # the same with packed `work` rows (RSL_WORK_PACK=1)
 }
 
 
-def _run(ctx, ch, cube, dyn):
+def _run(ctx, ch, cube, dyn, pack=False):
     old = os.environ.get('RSL_RF_DYN')
     os.environ['RSL_RF_DYN'] = dyn
+    old_pack = os.environ.get('RSL_WORK_PACK')
+    os.environ['RSL_WORK_PACK'] = '1' if pack else '0'
     try:
         ch.work.zero_()
         ch.rds.zero_()
@@ -34,6 +37,10 @@ def _run(ctx, ch, cube, dyn):
             os.environ.pop('RSL_RF_DYN', None)
         else:
             os.environ['RSL_RF_DYN'] = old
+        if old_pack is None:
+            os.environ.pop('RSL_WORK_PACK', None)
+        else:
+            os.environ['RSL_WORK_PACK'] = old_pack
     return [t.clone() for t in (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow)]
 
 
@@ -53,9 +60,10 @@ def test_dequeue_matches_static_walk(ctx, name):
     g = torch.Generator(device='cuda').manual_seed(7)
     cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
                          torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
-    ref = _run(ctx, ch, cube, '0')
+    pack = name.endswith('_pack')
+    ref = _run(ctx, ch, cube, '0', pack)
     assert ref[1].abs().amax().item() > 0
     for rep in range(21):
-        got = _run(ctx, ch, cube, '1')
+        got = _run(ctx, ch, cube, '1', pack)
         for a, b, what in zip(ref, got, ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
             assert torch.equal(_bits(a), _bits(b)), f'{name}: {what} differs on launch {rep}'
