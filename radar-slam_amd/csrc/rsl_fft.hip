@@ -1203,7 +1203,7 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
 
 // Packed `work` between K1 and K2 (see pk_pack): opt-in (RSL_WORK_PACK=1) where both kernels take their packed forms:
 // S = 512 (one bin pair per K1 thread), C = 128 (KB = 16 Doppler tiles), no tuning overrides.  Measured neutral
-// (tools: bench A/B, one call, 2 rounds: 197.9-198.1 k vs 197.3-198.4 k frames/s; K1 2.83-2.87 vs 2.90-2.95 ms,
+// (tools/pack_ab.sh, one call, 2 rounds: 197.9-198.1 k vs 197.3-198.4 k frames/s; K1 2.83-2.87 vs 2.90-2.95 ms,
 // K2 3.61-3.63 vs 3.50 ms per 2000 cfg2 frames): 25 % fewer `work` bytes do not shorten kernels bound by requests
 // in flight, and the c64 rows keep fp32 rounding, so c64 stays the default.
 bool work_pack_ok(int C, int S) {
