@@ -70,10 +70,6 @@ int rsl_fft_supported(int n);
 int rsl_timing_enable(rsl_handle h, int on);
 int rsl_timing_reset(rsl_handle h);
 int rsl_timing_read(rsl_handle h, int kernel_id, double* total_ms, long long* launches);
-/* Health word of the one-launch RDS path (rsl_rds_detect with the L2 ring, RSL_RING=1): the number of launches on
- * this handle's device that left an XCD's queue undrained or timed out a hand-off wait since the process started
- * (0 on a healthy device; synchronises the device). */
-long long rsl_ring_faults(rsl_handle h);
 
 /* a7  SignalPreprocessor.generate_range_doppler_spectrum  (dechirp.py:168-213, incl. process_chirp
  *     :143-166, dechirp_signal :122-141, apply_window :85-108, remove_dc :110-120, chirp_subset :183-187).

@@ -226,47 +226,17 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   bool sup = true;
   int group = 1;
   hipError_t e;
-  if (!db_map && rsl::rds_ring_supported(C, S) && getenv("RSL_RING") && atoi(getenv("RSL_RING")) != 0) {
-    {
-      Scope sc(h, RSL_K_RANGE_FFT);
-      e = rsl::launch_rds_ring(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                               tC, dc_removal, (float2*)work, (float2*)rds, thr_power, i_lo, i_hi,
-                               (unsigned long long*)mask, (int*)row_count, (float*)peak_pow, &group, &sup);
-    }
-    if (sup) {
-      if (peak_pow_group) *peak_pow_group = group;
-      return hip_check(h, e, "rds_ring");
-    }
-  }
-  if (!db_map && rsl::rds_fused_supported(C, S)) {  // one pass over the cube; `work` holds the Doppler 3-max
-    {
-      Scope sc(h, RSL_K_RANGE_FFT);
-      e = rsl::launch_rds_fused(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                                tC, dc_removal, (float2*)rds, work, thr_power, i_lo, i_hi);
-    }
-    if (int r = hip_check(h, e, "rds_fused")) return r;
-    {
-      Scope sc(h, RSL_K_DOPPLER_FFT);
-      e = rsl::launch_detect_finish(h->stream, work, F, A, C, S, (unsigned long long*)mask, (int*)row_count,
-                                    (float*)peak_pow, &group);
-    }
-    if (peak_pow_group) *peak_pow_group = group;
-    return hip_check(h, e, "detect_finish");
-  }
-  // packed range spectra between K1 and K2 (6 B per value; the exponents after the packed rows, inside the c64-sized
-  // work buffer the caller provides)
-  signed char* wexp = rsl::work_pack_ok(C, S) ? (signed char*)work + (size_t)F * A * C * S * 6 : nullptr;
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                              dc_removal, (float2*)work, &sup, wexp);
+                              dc_removal, (float2*)work, &sup);
   }
   if (int r = hip_check(h, e, "range_fft")) return r;
   {
     Scope sc(h, RSL_K_DOPPLER_FFT);
     e = rsl::launch_doppler_detect(h->stream, (const float2*)work, F, A, C, S, tC, (float2*)rds, thr_power, i_lo,
                                    i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
-                                   (float*)peak_pow, &sup, &group, wexp);
+                                   (float*)peak_pow, &sup, &group);
   }
   if (peak_pow_group) *peak_pow_group = group;
   return hip_check(h, e, "doppler_detect");
@@ -410,7 +380,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   Scope sc(h, RSL_K_DOA_SCAN);
   // the Toeplitz f16-MFMA scan: argmax only, or with the whole spectrum in the cell-blocked layout (no gmax there)
   const bool toep_spec = out_spec && (method & RSL_DOA_SPEC_BLOCKED) && !out_gmax;
-  if (toep && (!out_spec || toep_spec) && rsl::toep_table_fits(G, A) && getenv("RSL_DOA_FULL") == nullptr) {
+  if (toep && (!out_spec || toep_spec) && rsl::toep_table_fits(G, A)) {
     int nt32 = (G + 31) / 32;
     nt32 += nt32 & 1;
     const float* tp = (const float*)steer_tab + steer_f32_floats(G, A);
@@ -428,7 +398,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
                    rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
                                         (const long long*)ncell_dev, ncell, (const float*)steer_tab, ntiles, G,
                                         music, (int*)out_idx, (float*)out_gmax, (float*)out_spec,
-                                        (method & RSL_DOA_SPEC_BLOCKED) ? 1 : (method & RSL_DOA_SPEC_GMAJOR) ? ncell : 0,
+                                        (method & RSL_DOA_SPEC_BLOCKED) ? -1 : (method & RSL_DOA_SPEC_GMAJOR) ? ncell : 0,
                                         (int)blocks),
                    "doa_scan");
 }
@@ -652,13 +622,6 @@ int rsl_synth_cube(rsl_handle h, const void* pattern, int F, int A, int C, int S
                    rsl::launch_synth_cube(h->stream, (const double2*)pattern, F, A, C, S, noise_power, seed, frame0,
                                           (float2*)cube),
                    "synth_cube");
-}
-
-long long rsl_ring_faults(rsl_handle h) {
-  if (!h) return -1;
-  hipSetDevice(h->device);
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  return (long long)rsl::ring_faults();
 }
 
 long long rsl_pose_error_scratch_bytes(long long n, int nlen) {

@@ -485,9 +485,8 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   if (A > 32) return hipErrorInvalidValue;
   const int W = (C + 63) / 64;
   const long long nbe = ((long long)F * A * S * W + 255) / 256;
-  // cells: k_emit_cells when its frame-aligned blocks tile the cell words (RSL_EMIT_CELLS=0: the word-per-thread path)
-  const char* ec = getenv("RSL_EMIT_CELLS");
-  const bool cells4 = ((long long)S * W) % kCellWords == 0 && !(ec && atoi(ec) == 0);
+  // cells: k_emit_cells when its frame-aligned blocks tile the cell words, else the word-per-thread path
+  const bool cells4 = ((long long)S * W) % kCellWords == 0;
   const long long nbc = cells4 ? 0 : ((long long)F * S * W + 255) / 256;
   const unsigned nb = (unsigned)(nbe + nbc);
   if (cells4) {
@@ -510,11 +509,9 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
     if (e != hipSuccess) return e;
   }
   // registers capped for 7 waves per SIMD (72 VGPRs, no spill; 7 workgroups per CU as the LDS allows, instead of 6):
-  // emit 0.45-0.47 vs 0.46-0.48 ms per 1000 cfg2 frames (tools/cpb.sh); RSL_EMIT_WPE=0 for the unconstrained form
-  const char* ew = getenv("RSL_EMIT_WPE");
-  const int wpe = ew ? atoi(ew) : 7;
+  // emit 0.45-0.47 vs 0.46-0.48 ms per 1000 cfg2 frames (tools/cpb.sh)
 #define GO(WW)                                                                                                   \
-  hipLaunchKernelGGL((A <= 8 ? (wpe == 7 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 8>) : k_emit_block<WW, 32>),  \
+  hipLaunchKernelGGL((A <= 8 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 32>),                                   \
                      dim3(nb), dim3(256), 0, st, mask,                                                           \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
                      entry_cap, cell_cap, nbe, e_coord, e_cell, e_pdb, c_frame, c_rc, c_amask);
@@ -548,17 +545,9 @@ hipError_t launch_offsets(hipStream_t st, const unsigned long long* mask, const 
                           long long* cell_base, long long* frame_counts, unsigned long long* umask) {
   if (F <= 0) return hipSuccess;
   const int W = (C + 63) / 64;
-  static const int nt = [] {
-    const char* e = getenv("RSL_OFF_NT");
-    return e ? atoi(e) : 256;
-  }();
-  if (nt == 1024) {
-    hipLaunchKernelGGL(k_offsets<1024>, dim3(F), dim3(1024), 0, st, mask, row_count, A, S, W, entry_row_off,
-                       cell_row_off, cell_row_cnt, frame_counts, umask);
-  } else {
-    hipLaunchKernelGGL(k_offsets<256>, dim3(F), dim3(256), 0, st, mask, row_count, A, S, W, entry_row_off,
-                       cell_row_off, cell_row_cnt, frame_counts, umask);
-  }
+  // 256-thread blocks: 1024-thread ones waited for a whole CU to drain behind the other batch's DoA blocks
+  hipLaunchKernelGGL(k_offsets<256>, dim3(F), dim3(256), 0, st, mask, row_count, A, S, W, entry_row_off, cell_row_off,
+                     cell_row_cnt, frame_counts, umask);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_frame_scan<256>, dim3(1), dim3(256), 0, st, frame_counts, F, entry_base, cell_base);

@@ -159,8 +159,8 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
               const float d = (pz[t2] > 0.f) ? Mf - gv : (Mf - 1.f);
               val = (d > 1e-12f) ? __builtin_amdgcn_rcpf(d) : 0.f;  // angle_estimation.py:149-152 (v_rcp_f32: 1 ulp)
             }
-            if (spec_ld > 0) {
-              // grid-major: stage the tile (8 grid points x 32 cells) in LDS, stored below as 128-B runs
+            if (spec_ld != 0) {
+              // grid-major / cell-blocked: stage the tile (8 grid points x 32 cells) in LDS, stored below as 128-B runs
               reinterpret_cast<float*>(sstage + wave * 64)[(2 * q + h) * 32 + t2 * 16 + jj] = val;
             } else if (ok[t2] && g < G) {  // cell-major [n][G] (the reference's per-target spectrum rows)
               out_spec[(size_t)cidx[t2] * G + g] = val;
@@ -169,14 +169,14 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
         }
       }
       if constexpr (SPEC) {
-        if (spec_ld > 0) {
+        if (spec_ld != 0) {
           __builtin_amdgcn_wave_barrier();
           const int r = lane >> 3, c4 = lane & 7;  // grid point 8 t + r, cells 4 c4 .. 4 c4 + 3 of the chunk
           const float4 v = sstage[wave * 64 + r * 8 + c4];
           __builtin_amdgcn_wave_barrier();
           const int g = 8 * t + r;
           const long long c0 = ch * 32 + 4 * c4;
-          if (g < G && spec_ld == 1) {
+          if (g < G && spec_ld < 0) {
             // cell-blocked [ceil(n / 32)][G][32]: a tile is one contiguous 1 KiB run, a pass one 46 KiB block
             *reinterpret_cast<float4*>(out_spec + ((size_t)ch * G + g) * 32 + 4 * c4) = v;
           } else if (g < G) {
@@ -438,7 +438,7 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
   const size_t lds = use_lds ? tab_bytes : 0;
   const float4* stp = reinterpret_cast<const float4*>(steer_tab);
   const bool fast = (A == 2 * KS);
-  if (!out_spec && getenv("RSL_DOA_FULL") == nullptr) {  // argmax-only fast path
+  if (!out_spec) {  // argmax-only fast path
     const bool gm = out_gmax != nullptr;
 #define AM(n, F_)                                                                                                  \
   return music ? (gm ? launch_argmax_t<n, F_, true, true>(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host,  \

@@ -604,15 +604,12 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
                                 double esprit_scale, double* out_esprit, double* out_phase, int max_blocks,
                                 float* out_spec = nullptr) {
   auto kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 0, false, SPEC>;
-  if constexpr (MA == 8) {  // the 0.5-degree grid (G = 361: 12 tiles of 32): unrolled tile loop
-    const char* eu = getenv("RSL_DOA_UNROLL");
-    // skewed column-tile chains (default; RSL_DOA_SKEW=0 for the plain order): tools/doa_var_ab.py, one call,
-    // 3.77-3.78 vs 3.83-3.87 ms per 2000 cfg2 frames, outputs bit-identical
-    const char* es = getenv("RSL_DOA_SKEW");
-    const bool skew = !es || atoi(es) != 0;
-    if (ntiles == 12 && (!eu || atoi(eu) != 0) && !SPEC)  // the spectrum scan keeps the rolled tile loop
-      kern = skew ? k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true> : k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12>;
+  if constexpr (MA == 8 && !SPEC) {  // the 0.5-degree grid (G = 361: 12 tiles of 32): unrolled tile loop
+    // skewed column-tile chains: tools/doa_var_ab.py, one call, 3.77-3.78 vs 3.83-3.87 ms per 2000 cfg2 frames,
+    // outputs bit-identical (the spectrum scan keeps the rolled tile loop: the unrolled one spills with the stores)
+    if (ntiles == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true>;
   }
+#ifdef RSL_DEV_KNOBS
   if constexpr (MUSIC && !GMAX && !EXTRAS && !SPEC && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing only)
     if (const char* e = getenv("RSL_DOA_DBG")) {
       const int v = atoi(e);
@@ -625,23 +622,15 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
       }
     }
   }
+#endif
   const size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);
   if (lds > 64 * 1024) return hipErrorInvalidValue;  // caller checks toep_table_fits()
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
-  if (const char* e = getenv("RSL_DOA_BPC"))  // blocks-per-CU cap: leaves room for a concurrent kernel (pipelined chain)
-    if (atoi(e) > 0 && atoi(e) < nb) nb = atoi(e);
-  int dev = 0, ncu = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  long long blocks = (long long)nb * ncu;
-  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+  (void)max_blocks;
   // Grid sized from the cell count (the capacity when the count is on the device; blocks past the cells exit before
   // loading the table) with ~8 passes per wave, instead of a persistent grid of resident blocks: measured 1.52-1.56
-  // vs 1.71-1.79 ms per 1000 cfg2 frames.  RSL_DOA_PPW=0 restores the persistent grid.
-  const char* eppw = getenv("RSL_DOA_PPW");
-  const int ppw = eppw ? atoi(eppw) : 8;
-  if (ppw > 0) blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
+  // vs 1.71-1.79 ms per 1000 cfg2 frames (4 or 16 passes per wave: no better, tools/ppw_ab.sh).
+  constexpr long long ppw = 8;
+  long long blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
                      ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,

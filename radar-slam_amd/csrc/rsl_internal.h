@@ -16,8 +16,7 @@ __device__ __forceinline__ long long list_count(const long long* dev, long long 
 // K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
 // cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
-                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
-                            signed char* wexp = nullptr);
+                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported);
 // K2: Doppler FFT (C points) + fftshift on both axes, transposed store.
 // work c64 [F, A, C, S] -> rds c64 [F, A, S, C]
 hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
@@ -29,29 +28,7 @@ bool doppler_detect_supported(int C, int S);
 float threshold_as_float(double thr);  // largest float t <= thr
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group,
-                                 const signed char* wexp = nullptr);
-// wexp non-null (both launches): `work` holds packed rows (24-bit mantissas, int8 exponents at wexp; rsl_fft.hip
-// pk_pack) instead of c64 -- only where work_pack_ok(C, S).
-bool work_pack_ok(int C, int S);
-// K12 + K3' (rsl_rds_fused.hip): one-pass range + Doppler FFT per (slab, range class) with the Doppler-direction half
-// of detection (Doppler 3-max + candidate bits into `work`), then the range-direction finish -> the same mask /
-// row_count / tile-compact peak powers as launch_doppler_detect.  S = 512, C = 128; opt-in with RSL_FUSED=1 (slower).
-bool rds_fused_supported(int C, int S);
-// K1 + K2 in one persistent launch with `work` as a per-XCD ring of slabs held in L2 (rsl_fft.hip; S = 512, C = 128,
-// an 8-XCC device).  Outputs as launch_doppler_detect (tile-compact peak powers, group KB).  ring_faults(): launches
-// that left a queue undrained or timed out a wait (0 on a healthy run).
-bool rds_ring_supported(int C, int S);
-hipError_t launch_rds_ring(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
-                           const float2* table, const float2* twS, const float2* twC, int dc, float2* work,
-                           float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
-                           float* pk_pow, int* pk_group, bool* supported);
-unsigned ring_faults();
-hipError_t launch_rds_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
-                            const float2* table, const float2* tw_S, const float2* tw_C, int dc, float2* rds,
-                            void* work, double thr_p, int i_lo, int i_hi);
-hipError_t launch_detect_finish(hipStream_t st, const void* work, int F, int A, int C, int S,
-                                unsigned long long* mask, int* row_count, float* pk_pow, int* pk_group);
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);

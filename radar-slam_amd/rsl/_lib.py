@@ -67,7 +67,6 @@ SIGNATURES = {
     'rsl_synth_pattern': (c_int, [_P, _P, c_int, c_int, c_int, c_double, c_double, c_double, c_double, _P]),
     'rsl_synth_cube': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_ulonglong, c_longlong, _P]),
     'rsl_pose_error_scratch_bytes': (c_longlong, [c_longlong, c_int]),
-    'rsl_ring_faults': (c_longlong, [c_void_p]),
     'rsl_music_subspace': (c_int, [_P, _P, c_longlong, c_int, c_int, _P, c_int, _P]),
     'rsl_esprit_subspace': (c_int, [_P, _P, c_longlong, c_int, c_int, c_double, _P]),
     'rsl_pose_align': (c_int, [_P, _P, _P, c_longlong, _P, _P, _P, _P, _P]),

@@ -34,6 +34,27 @@ def test_library_exports_header():
     assert lib.rsl_version() == 1
 
 
+def test_library_reads_no_environment():
+    """The product librsl.so selects no kernel variant from its caller's environment: it does not
+    import getenv / secure_getenv at all.  The ablation switches exist only in the development build
+    (make dev -> librsl_dev.so, -DRSL_DEV_KNOBS), which the runtime loads only when RSL_LIBRARY names it."""
+    import subprocess
+    from rsl import _lib
+    path = os.path.join(ROOT, 'radar-slam_amd', 'lib', 'librsl.so')
+    assert os.path.abspath(_lib.LIB_PATH) == os.path.abspath(path) or 'RSL_LIBRARY' in os.environ
+    out = subprocess.run(['nm', '-D', '--undefined-only', path], capture_output=True, text=True, check=True).stdout
+    syms = {ln.split()[-1].split('@')[0] for ln in out.splitlines() if ln.strip()}
+    assert not syms & {'getenv', 'secure_getenv', '__secure_getenv'}, sorted(syms & {'getenv', 'secure_getenv'})
+    srcs = os.path.join(ROOT, 'radar-slam_amd', 'csrc')
+    for fn in sorted(os.listdir(srcs)):
+        if fn.endswith(('.hip', '.h')):
+            src = open(os.path.join(srcs, fn)).read()
+            # every getenv in the kernel sources sits inside an RSL_DEV_KNOBS block
+            for m in re.finditer(r'getenv\(', src):
+                head = src[:m.start()]
+                assert head.rfind('#ifdef RSL_DEV_KNOBS') > head.rfind('#endif'), f'{fn}: getenv outside RSL_DEV_KNOBS'
+
+
 def test_fft_support_table():
     import rsl
     lib = rsl.load()

@@ -3,7 +3,6 @@
 Cubes come from the oracle's restatement of simulate_raw.synthesize_frame (bit-identical to the
 reference, pinned in test_oracle_golden.py) and are fed to the GPU as complex64.
 """
-import os
 
 import numpy as np
 import pytest
@@ -20,10 +19,6 @@ CFGS = {  # name: (A, C, T_c)
     'cfg2': (8, 128, 51.2e-6),
     'cfg5a16': (16, 32, 12.8e-6),
     'cfg5': (16, 256, 102.4e-6),  # configs[4] frame shape (A16 C256 S1024), one frame
-    'cfg2_onepass': (8, 128, 51.2e-6),  # the opt-in one-pass range-class RDS kernel (RSL_FUSED=1, rsl_rds_fused.hip)
-    'cfg2_ring': (8, 128, 51.2e-6),  # K1 + K2 in one launch with `work` as a per-XCD L2 ring (k_rds_ring, RSL_RING=1)
-    # K1 -> K2 range spectra as packed rows (24-bit mantissas, shared exponents; opt-in RSL_WORK_PACK=1)
-    'cfg2_packwork': (8, 128, 51.2e-6),
     'a4': (4, 64, 25.6e-6),  # fewer antennas than the DoA kernel's width (zero-padded signature, per-element ESPRIT)
     'cfg1_ridge': (8, 64, 25.6e-6),  # regularised LS velocity (ridge 0.01 on v, velocity_solver_improved.py:261)
 }
@@ -50,20 +45,8 @@ def runs(ctx):
         cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=RIDGE.get(name, 0.0))
         ch = rsl.RadarChain(cfg, F, ctx)
         cube = ctx.to_dev(frames.astype(np.complex64))
-        env = {'_onepass': ('RSL_FUSED', '1'), '_ring': ('RSL_RING', '1'), '_packwork': ('RSL_WORK_PACK', '1')}
-        key, val = next((v for k, v in env.items() if name.endswith(k)), (None, None))
-        old = os.environ.get(key) if key else None
-        if key:
-            os.environ[key] = val
-        try:
-            ch.run(cube)
-            res = ch.results()
-        finally:
-            if key:
-                if old is None:
-                    os.environ.pop(key, None)
-                else:
-                    os.environ[key] = old
+        ch.run(cube)
+        res = ch.results()
         res['rds'] = ch.rds.cpu().numpy()
         res['mask_words'] = ch.mask.cpu().numpy()
         res['frames'] = frames

@@ -88,6 +88,14 @@ def test_spectrum_layouts_agree(ctx):
     torch.cuda.synchronize()
     assert torch.equal(s_cm, s_gm.t())
     assert torch.equal(s_cm, spectrum_rows(s_bl, nc))
+    # grid-major with a leading dimension of 1, 2 or 3 cells: the layout is a flag of its own, so ld = 1 is not taken
+    # for the cell-blocked layout (which would write G * 32 floats into a [G][1] buffer)
+    for n in (1, 2, 3):
+        _, _, s1 = ctx.doa(ch.rds, L['c_frame'], L['c_rc'], ch.steer, ch.method, n=n, want_spec=True,
+                           spec_gmajor=True, fast=False)
+        torch.cuda.synchronize()
+        assert tuple(s1.shape) == (len(ch.grid), n)
+        assert torch.equal(s_cm[:n], s1.t())
 
 
 @pytest.mark.parametrize('method', ['music', 'beamforming'])
