@@ -217,6 +217,28 @@ int rsl_bvls(rsl_handle h, const void* pos, const void* ang, long long n, const 
 int rsl_associate(rsl_handle h, const void* cur_xy, int nc, const void* prev_xy, int np, double thr, void* scratch,
                   void* match, void* dist);
 
+/* configs[3] per-frame pattern, peak selection of RobustAngleEstimator.process_targets_robust
+ *     (robust_angle_estimation.py:362-369: power_db > thr_db, stable sort by power_db descending, first kmax), for
+ *     every cube k of a batch at once.  entry_base i64 [ncube + 1], e_coord u32 / e_pdb f32 [entry_cap] are the
+ *     chain's compacted entries (rsl_peak_emit); kmax <= 256.  Outputs (device, slots k * kmax + r): sel_entry i32
+ *     (global entry index, -1 past the selection), sel_frame i32 (= k) and sel_rc i32 (range_bin * C + doppler_bin;
+ *     a DoA cell list for rsl_doa / rsl_confidence / rsl_cell_extras), sel_n i32 [ncube] = selected count.  The
+ *     selection is in the reference's order: power descending, ties in entry (antenna -> range -> Doppler) order. */
+int rsl_peak_topk(rsl_handle h, const void* entry_base, long long entry_cap, int ncube, const void* e_coord,
+                  const void* e_pdb, double thr_db, int kmax, int C, void* sel_entry, void* sel_frame, void* sel_rc,
+                  void* sel_n);
+
+/* configs[3] per-frame pattern: CompleteRadarScenesAnalyzer._create_target_associations
+ *     (radarscenes_complete_analysis.py:274-305) for every frame of a batch at once.  Targets of frame f are
+ *     [off[f], off[f+1]) of the concatenated f64 arrays range_m, az_rad and s0 (c128: the first component of each
+ *     target's spatial signature); off i64 [nframes + 1] on the device.  For target i of frame f > 0: the target j of
+ *     frame f-1 with the smallest sqrt((r_i - r_j)^2 + (az_i - az_j)^2), strict '<' against the running minimum and
+ *     against thr (first minimum wins; previous targets may be matched many times), in exact float64.  Outputs
+ *     [off[nframes]]: match i32 (index within frame f-1, -1 = none; always -1 in frame 0), dist f64, phase f64 =
+ *     angle(s0_i * conj(s0_j)) (:296; 0 where unmatched). */
+int rsl_associate_nearest(rsl_handle h, const void* range_m, const void* az_rad, const void* s0, const void* off,
+                          int nframes, long long ntargets, double thr, void* match, void* dist, void* phase);
+
 /* a30, a31  wrapped-phase ego-motion solve: minimises sum_i wrap(y_i - k J_i.x)^2 + R(x) over the box
  *     [lo6, hi6] (host), J_i = [d_i, p_i x d_i] from pos f64 [n][3] and ang f64 [n][2] (az, el).
  *     mode 0: R = 0.01 |v|^2 + 0.01 |w|^2 (velocity_solver_improved.py:223-266);
@@ -226,10 +248,25 @@ int rsl_associate(rsl_handle h, const void* cur_xy, int nc, const void* prev_xy,
  *     over (v_x, v_y) plus nextra extra starts extra f64 [nextra][6] (device), iters iterations each;
  *     out f64 [8] (device) = {x[6], cost, start index}.  scratch >= rsl_wrapped_scratch_bytes(n, grid_n, nextra). */
 long long rsl_wrapped_scratch_bytes(long long n, int grid_n, int nextra);
+
 int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int mode,
                       double w, double vmax, double wmax, const void* prev, const double* lo6, const double* hi6,
                       int nv, int grid_n, const void* extra, int nextra, int iters, void* scratch,
                       long long scratch_bytes, void* out);
+
+/* a30, a31  the same minimisation with a basin-resolving global stage (cost <= the reference DE).
+ *     Stage 1: projected 2-D Gauss-Newton in (x0, x1) = (v_x, v_y) from every point of a grid with the given spacing
+ *     (a fraction of the wrap period 2 pi / k; ceil(width / spacing) points per axis, at most 32768) over
+ *     [lo6[0], hi6[0]] x [lo6[1], hi6[1]], with x[2..5] held at base6 (host, clipped to the box; the regulariser's
+ *     optimum for them); stage 2: the nv-D Gauss-Newton of rsl_wrapped_solve from the nbest best stage-1 minima
+ *     (1..1024) and the extra starts.  out as rsl_wrapped_solve (start index = position among the stage-2 starts).
+ *     scratch >= rsl_wrapped_search_scratch_bytes(n, lo6, hi6, spacing, nbest, nextra). */
+long long rsl_wrapped_search_scratch_bytes(long long n, const double* lo6, const double* hi6, double spacing,
+                                           int nbest, int nextra);
+int rsl_wrapped_search(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int mode,
+                       double w, double vmax, double wmax, const void* prev, const double* lo6, const double* hi6,
+                       int nv, const double* base6, double spacing, int nbest, const void* extra, int nextra, int iters,
+                       void* scratch, long long scratch_bytes, void* out);
 
 /* L4 trajectory  PoseIntegrator.integrate_translational_velocity / integrate_angular_velocity
  *     (pose_integration.py:67-167) as block-wide fp64 prefix scans over one frame block.

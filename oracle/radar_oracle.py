@@ -478,6 +478,25 @@ def associate_greedy(cur_xy, prev_xy, thr=5.0):
     return match, dist
 
 
+def associate_analyzer(cur_r, cur_az, prev_r, prev_az, thr=5.0):
+    """CompleteRadarScenesAnalyzer._create_target_associations (results/ground_truth_comparison/
+    radarscenes_complete_analysis.py:274-305): for each current target in order, the previous target with the smallest
+    sqrt((r - r')^2 + (az - az')^2) (metres and radians mixed) under a strict '<' against the running minimum and
+    against thr; previous targets may be used many times.  Returns (match [Nc] with -1 = none, dist [Nc])."""
+    cur_r, cur_az = np.asarray(cur_r, np.float64), np.asarray(cur_az, np.float64)
+    prev_r, prev_az = np.asarray(prev_r, np.float64), np.asarray(prev_az, np.float64)
+    match = np.full(len(cur_r), -1, np.int64)
+    dist = np.full(len(cur_r), np.inf)
+    for i in range(len(cur_r)):
+        best = float('inf')
+        for j in range(len(prev_r)):
+            d = np.sqrt((cur_r[i] - prev_r[j]) ** 2 + (cur_az[i] - prev_az[j]) ** 2)
+            if d < best and d < thr:
+                best, match[i] = d, j
+        dist[i] = best
+    return match, dist
+
+
 def phase_pred(x6, pos, ang, k):
     """k (v + w x p).d, d = (cos el cos az, cos el sin az, sin el) (velocity_solver_improved.py:173-221)."""
     az, el = ang[:, 0], ang[:, 1]

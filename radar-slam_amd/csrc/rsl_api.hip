@@ -526,6 +526,43 @@ int rsl_associate(rsl_handle h, const void* cur_xy, int nc, const void* prev_xy,
                    "associate");
 }
 
+int rsl_peak_topk(rsl_handle h, const void* entry_base, long long entry_cap, int ncube, const void* e_coord,
+                  const void* e_pdb, double thr_db, int kmax, int C, void* sel_entry, void* sel_frame, void* sel_rc,
+                  void* sel_n) {
+  if (!h) return RSL_ERR_INVALID;
+  if (ncube < 0 || entry_cap < 0 || C <= 0 || C > 8192) return fail(h, RSL_ERR_INVALID, "rsl_peak_topk: bad argument");
+  if (kmax < 1 || kmax > 256) return fail(h, RSL_ERR_UNSUPPORTED, "rsl_peak_topk: kmax must be 1..256");
+  if (ncube == 0) return RSL_OK;
+  if (!entry_base || !sel_entry || !sel_frame || !sel_rc || !sel_n || (entry_cap > 0 && (!e_coord || !e_pdb)))
+    return fail(h, RSL_ERR_INVALID, "rsl_peak_topk: null pointer");
+  hipSetDevice(h->device);
+  Scope sc(h, RSL_K_AUX);
+  // the reference compares float64 power_db > thr_db; the entries' power_db is f32, so compare against the largest
+  // float <= thr_db (identical decisions for every f32 value)
+  return hip_check(h,
+                   rsl::launch_topk_entries(h->stream, (const long long*)entry_base, entry_cap, ncube,
+                                            (const unsigned*)e_coord, (const float*)e_pdb,
+                                            rsl::threshold_as_float(thr_db), kmax, C, (int*)sel_entry,
+                                            (int*)sel_frame, (int*)sel_rc, (int*)sel_n),
+                   "peak_topk");
+}
+
+int rsl_associate_nearest(rsl_handle h, const void* range_m, const void* az_rad, const void* s0, const void* off,
+                          int nframes, long long ntargets, double thr, void* match, void* dist, void* phase) {
+  if (!h) return RSL_ERR_INVALID;
+  if (nframes < 0 || ntargets < 0 || !(thr >= 0)) return fail(h, RSL_ERR_INVALID, "rsl_associate_nearest: bad argument");
+  if (nframes == 0 || ntargets == 0) return RSL_OK;
+  if (!range_m || !az_rad || !s0 || !off || !match || !dist || !phase)
+    return fail(h, RSL_ERR_INVALID, "rsl_associate_nearest: null pointer");
+  hipSetDevice(h->device);
+  Scope sc(h, RSL_K_AUX);
+  return hip_check(h,
+                   rsl::launch_associate_nearest(h->stream, (const double*)range_m, (const double*)az_rad,
+                                                 (const double2*)s0, (const long long*)off, nframes, ntargets, thr,
+                                                 (int*)match, (double*)dist, (double*)phase),
+                   "associate_nearest");
+}
+
 long long rsl_wrapped_scratch_bytes(long long n, int grid_n, int nextra) {
   if (n < 0 || grid_n < 0 || nextra < 0) return -1;
   return 8LL * (6 * n + 36 + 8 * ((long long)grid_n * grid_n + nextra));
@@ -551,6 +588,53 @@ int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long 
                                              k, mode, w, vmax, wmax, (const double*)prev, lo6, hi6, nv, grid_n,
                                              (const double*)extra, nextra, iters, (double*)scratch, (double*)out),
                    "wrapped_solve");
+}
+
+// stage-1 grid of rsl_wrapped_search: ceil(width / spacing) points per axis, at least 1, at most 2^15 (so the grid
+// has < 2^30 starts)
+static void search_grid(const double* lo6, const double* hi6, double spacing, long long* gx, long long* gy) {
+  auto pts = [&](double w) {
+    double g = spacing > 0 ? ceil(w / spacing) : 1.0;
+    if (!(g >= 1.0)) g = 1.0;
+    if (g > 32768.0) g = 32768.0;
+    return (long long)g;
+  };
+  *gx = pts(hi6[0] - lo6[0]);
+  *gy = pts(hi6[1] - lo6[1]);
+}
+
+long long rsl_wrapped_search_scratch_bytes(long long n, const double* lo6, const double* hi6, double spacing,
+                                           int nbest, int nextra) {
+  if (n < 0 || !lo6 || !hi6 || nbest < 1 || nextra < 0) return -1;
+  long long gx, gy;
+  search_grid(lo6, hi6, spacing, &gx, &gy);
+  return 8LL * rsl::wrapped_search_scratch_doubles(n, gx * gy, nbest, nextra);
+}
+
+int rsl_wrapped_search(rsl_handle h, const void* pos, const void* ang, long long n, const void* y, double k, int mode,
+                       double w, double vmax, double wmax, const void* prev, const double* lo6, const double* hi6,
+                       int nv, const double* base6, double spacing, int nbest, const void* extra, int nextra, int iters,
+                       void* scratch, long long scratch_bytes, void* out) {
+  if (!h) return RSL_ERR_INVALID;
+  if (n < 1 || (nv != 3 && nv != 6) || (mode != 0 && mode != 1) || !(spacing > 0) || nbest < 1 || nbest > 1024 ||
+      nextra < 0 || iters < 0)
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_search: bad argument");
+  if (!pos || !ang || !y || !lo6 || !hi6 || !base6 || !scratch || !out || (nextra > 0 && !extra))
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_search: null pointer");
+  for (int a = 0; a < 6; ++a)
+    if (!(lo6[a] <= hi6[a])) return fail(h, RSL_ERR_INVALID, "rsl_wrapped_search: bad bounds");
+  if (scratch_bytes < rsl_wrapped_search_scratch_bytes(n, lo6, hi6, spacing, nbest, nextra))
+    return fail(h, RSL_ERR_INVALID, "rsl_wrapped_search: scratch too small");
+  long long gx, gy;
+  search_grid(lo6, hi6, spacing, &gx, &gy);
+  hipSetDevice(h->device);
+  Scope sc(h, RSL_K_VELOCITY);
+  return hip_check(h,
+                   rsl::launch_wrapped_search(h->stream, (const double*)pos, (const double*)ang, n, (const double*)y,
+                                              k, mode, w, vmax, wmax, (const double*)prev, lo6, hi6, nv, base6, gx,
+                                              gy, nbest, (const double*)extra, nextra, iters, (double*)scratch,
+                                              (double*)out),
+                   "wrapped_search");
 }
 
 int rsl_traj_scan(rsl_handle h, const void* vel, int vstride, int nv, const void* omega, int ostride,

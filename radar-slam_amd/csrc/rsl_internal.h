@@ -78,8 +78,20 @@ hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, co
                            const double* bounds4, double* out, double* resid, double* pred);
 
 // K9: greedy association and wrapped-phase multi-start solve (rsl_wrap.hip).
+// configs[3] pattern (rsl_scene.hip): per-cube top-k peak selection and the analyser's nearest association.
+hipError_t launch_topk_entries(hipStream_t st, const long long* entry_base, long long entry_cap, int ncube,
+                               const unsigned* e_coord, const float* e_pdb, float thr_db, int kmax, int C,
+                               int* sel_entry, int* sel_frame, int* sel_rc, int* sel_n);
+hipError_t launch_associate_nearest(hipStream_t st, const double* range_m, const double* az_rad, const double2* s0,
+                                    const long long* off, int nframes, long long ntargets, double thr, int* match,
+                                    double* dist, double* phase);
 hipError_t launch_associate(hipStream_t st, const double* cur, int nc, const double* prev, int np, double thr,
                             unsigned* used_scratch, int* match, double* dist);
+long wrapped_search_scratch_doubles(long n, long nstart1, int nbest, int nextra);
+hipError_t launch_wrapped_search(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
+                                 double k, int mode, double w, double vmax, double wmax, const double* prev,
+                                 const double* lo, const double* hi, int nv, const double* base6, long gx, long gy,
+                                 int nbest, const double* extra, int nextra, int iters, double* scratch, double* out);
 hipError_t launch_wrapped_solve(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
                                 double k, int mode, double w, double vmax, double wmax, const double* prev,
                                 const double* lo, const double* hi, int nv, int gn, const double* extra, int nextra,

@@ -351,6 +351,252 @@ __global__ __launch_bounds__(256) void k_wrapped_jac(const double* __restrict__ 
   o[5] = px * d1 - py * d0;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Dense wrapped search.  The wrapped cost is a sum of N periodic ridges, period 2 pi / (k |J_i|) along each target's
+// J_i (0.0195 m/s in radial velocity at 77 GHz and dt = 0.1): a glassy landscape with millions of basins over the
+// velocity box, which a coarse multi-start grid samples only in part.  Stage 1 runs a projected 2-D Gauss-Newton in
+// (x0, x1) = (v_x, v_y) -- the coordinates the data term depends on for the reference's geometry (elevation 0 and
+// p = r d make (w x p).d = 0 and d_z = 0: SURVEY §0 fact 8) -- from every point of a grid whose spacing is a fraction
+// of the wrap period, so every basin the grid resolves is entered; x[2..5] are held at base (the regulariser's
+// optimum for them).  Each block keeps its best start; the best nbest blocks seed stage 2, the full nv-D Gauss-Newton
+// of k_wrapped_ms, together with the caller's extra starts.
+// ---------------------------------------------------------------------------------------------------------
+// Per-target stage-1 terms: (J_i0, J_i1, y_i - k sum_{a >= 2} J_ia base_a).
+__global__ __launch_bounds__(256) void k_wrapped_prep2(const double* __restrict__ J, const double* __restrict__ y,
+                                                       long n, double k, const double* __restrict__ base,
+                                                       double* __restrict__ T) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double* Ji = J + 6 * i;
+  double c = 0.0;
+  for (int a = 2; a < 6; ++a) c += Ji[a] * base[a];
+  T[3 * i] = Ji[0];
+  T[3 * i + 1] = Ji[1];
+  T[3 * i + 2] = y[i] - k * c;
+}
+
+struct Six {
+  double v[6];
+};
+__global__ void k_fill6(double* __restrict__ dst, Six s) {
+  if (threadIdx.x < 6) dst[threadIdx.x] = s.v[threadIdx.x];
+}
+
+struct Grid2 {
+  long gx, gy;
+  double x0, y0, hx, hy;  // start (ix, iy) = (x0 + (ix + 0.5) hx, y0 + (iy + 0.5) hy)
+};
+
+RSL_DEV double data_cost2(const double* __restrict__ T, long n, double k, double vx, double vy, double* g) {
+  double c = 0.0, g0 = 0.0, g1 = 0.0;
+  for (long i = 0; i < n; ++i) {
+    const double j0 = T[3 * i], j1 = T[3 * i + 1];
+    const double r = wrap_pi(T[3 * i + 2] - k * (j0 * vx + j1 * vy));
+    c += r * r;
+    g0 += j0 * r;
+    g1 += j1 * r;
+  }
+  if (g) {
+    g[0] = -2.0 * k * g0;
+    g[1] = -2.0 * k * g1;
+  }
+  return c;
+}
+
+RSL_DEV double data_cost2_f(const double* __restrict__ T, long n, double k, double vx, double vy) {
+  double c = 0.0;
+  for (long i = 0; i < n; ++i) {
+    const double r = wrap_pi(T[3 * i + 2] - k * (T[3 * i] * vx + T[3 * i + 1] * vy));
+    c += r * r;
+  }
+  return c;
+}
+
+// One grid start per thread; block result = (cost, x0, x1, start index) of its best start.
+__global__ __launch_bounds__(256) void k_wrapped_grid2(WrapProblem P, const double* __restrict__ T,
+                                                       const double* __restrict__ Hd, const double* __restrict__ base,
+                                                       Grid2 Gd, int iters, double* __restrict__ blk) {
+  __shared__ double sc[256], sx[256], sy[256];
+  __shared__ long si[256];
+  const int t = threadIdx.x;
+  const long s = (long)blockIdx.x * 256 + t;
+  const long nstart = Gd.gx * Gd.gy;
+  double f = INFINITY, x[6];
+  for (int a = 0; a < 6; ++a) x[a] = base[a];
+  if (s < nstart) {
+    const long ix = s % Gd.gx, iy = s / Gd.gx;
+    x[0] = fmin(fmax(Gd.x0 + ((double)ix + 0.5) * Gd.hx, P.lo[0]), P.hi[0]);
+    x[1] = fmin(fmax(Gd.y0 + ((double)iy + 0.5) * Gd.hy, P.lo[1]), P.hi[1]);
+    double g[2];
+    f = data_cost2(T, P.n, P.k, x[0], x[1], g) + reg_cost(P, x);
+    const double h00 = Hd[0], h01 = Hd[1], h11 = Hd[7];
+    for (int it = 0; it < iters; ++it) {
+      double gr[6], H[6][6];
+      reg_grad_hess(P, x, gr, H);
+      const double a = h00 + H[0][0], b = h01 + H[0][1], c = h11 + H[1][1];
+      const double g0 = g[0] + gr[0], g1 = g[1] + gr[1];
+      double det = a * c - b * b;
+      if (!(det > 1e-300)) det = 1e-300;
+      const double d0 = -(c * g0 - b * g1) / det, d1 = -(a * g1 - b * g0) / det;
+      double step = 1.0, fn = f, xn0 = x[0], xn1 = x[1];
+      bool ok = false;
+      for (int ls = 0; ls < 6; ++ls) {
+        xn0 = fmin(fmax(x[0] + step * d0, P.lo[0]), P.hi[0]);
+        xn1 = fmin(fmax(x[1] + step * d1, P.lo[1]), P.hi[1]);
+        const double xs0 = x[0], xs1 = x[1];
+        x[0] = xn0;
+        x[1] = xn1;
+        fn = data_cost2_f(T, P.n, P.k, xn0, xn1) + reg_cost(P, x);
+        x[0] = xs0;
+        x[1] = xs1;
+        if (fn < f) {
+          ok = true;
+          break;
+        }
+        step *= 0.5;
+      }
+      if (!ok) break;
+      const double df = f - fn;
+      x[0] = xn0;
+      x[1] = xn1;
+      f = fn;
+      if (df <= 1e-13 * (1.0 + f)) break;
+      data_cost2(T, P.n, P.k, x[0], x[1], g);
+    }
+  }
+  sc[t] = f;
+  sx[t] = x[0];
+  sy[t] = x[1];
+  si[t] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      const double oc = sc[t + off];
+      const long oi = si[t + off];
+      if (oc < sc[t] || (oc == sc[t] && oi < si[t])) {
+        sc[t] = oc;
+        sx[t] = sx[t + off];
+        sy[t] = sy[t + off];
+        si[t] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    double* o = blk + 4 * (long)blockIdx.x;
+    o[0] = sc[0];
+    o[1] = sx[0];
+    o[2] = sy[0];
+    o[3] = (double)si[0];
+  }
+}
+
+// The nbest lowest block results (cost, then start index), written as 6-D starts (x0, x1, base[2..5]) in front of
+// the caller's extra starts; taken entries are marked +inf.  One block.
+__global__ __launch_bounds__(1024) void k_wrapped_topk(double* __restrict__ blk, long nblk, int nbest,
+                                                       const double* __restrict__ base, double* __restrict__ starts) {
+  __shared__ double sc[1024];
+  __shared__ long si[1024];
+  const int t = threadIdx.x;
+  for (int q = 0; q < nbest; ++q) {
+    double bc = INFINITY;
+    long bi = -1;
+    for (long b = t; b < nblk; b += 1024) {
+      const double c = blk[4 * b];
+      const long idx = (long)blk[4 * b + 3];
+      if (c < bc || (c == bc && bi >= 0 && idx < (long)blk[4 * bi + 3])) {
+        bc = c;
+        bi = b;
+      }
+    }
+    sc[t] = bc;
+    si[t] = bi;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+      if (t < off) {
+        const double oc = sc[t + off];
+        const long ob = si[t + off];
+        if (ob >= 0 && (si[t] < 0 || oc < sc[t] ||
+                        (oc == sc[t] && (long)blk[4 * ob + 3] < (long)blk[4 * si[t] + 3]))) {
+          sc[t] = oc;
+          si[t] = ob;
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const long b = si[0];
+      double* o = starts + 6 * q;
+      o[0] = b >= 0 ? blk[4 * b + 1] : base[0];
+      o[1] = b >= 0 ? blk[4 * b + 2] : base[1];
+      for (int a = 2; a < 6; ++a) o[a] = base[a];
+      if (b >= 0) blk[4 * b] = INFINITY;
+    }
+    __syncthreads();
+  }
+}
+
+// scratch doubles of launch_wrapped_search: J [6n] | Hd [36] | T [3n] | base [6] | block results [4 nblk] |
+// starts [6 (nbest + nextra)] | per-start results [8 (nbest + nextra)]
+long wrapped_search_scratch_doubles(long n, long nstart1, int nbest, int nextra) {
+  const long nblk = (nstart1 + 255) / 256;
+  return 6 * n + 36 + 3 * n + 6 + 4 * nblk + 14L * (nbest + nextra);
+}
+
+hipError_t launch_wrapped_search(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
+                                 double k, int mode, double w, double vmax, double wmax, const double* prev,
+                                 const double* lo, const double* hi, int nv, const double* base6, long gx, long gy,
+                                 int nbest, const double* extra, int nextra, int iters, double* scratch, double* out) {
+  double* J = scratch;
+  double* Hd = J + 6 * n;
+  double* T = Hd + 36;
+  double* base = T + 3 * n;
+  double* blk = base + 6;
+  const long nstart1 = gx * gy;
+  const long nblk = (nstart1 + 255) / 256;
+  double* starts = blk + 4 * nblk;
+  double* res = starts + 6L * (nbest + nextra);
+  Six b6;
+  for (int a = 0; a < 6; ++a) b6.v[a] = fmin(fmax(base6[a], lo[a]), hi[a]);
+  hipLaunchKernelGGL(k_fill6, dim3(1), dim3(64), 0, st, base, b6);  // by value: no pageable host copy
+  if (nextra > 0) {
+    const hipError_t e = hipMemcpyAsync(starts + 6L * nbest, extra, 6 * sizeof(double) * nextra, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_wrapped_jac, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos, ang, n, J);
+  hipLaunchKernelGGL(k_wrapped_hess, dim3(1), dim3(256), 0, st, J, n, k, Hd);
+  hipLaunchKernelGGL(k_wrapped_prep2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, J, y, n, k, base, T);
+  WrapProblem P;
+  P.J = J;
+  P.y = y;
+  P.n = n;
+  P.k = k;
+  P.mode = mode;
+  P.w = w;
+  P.vmax = vmax;
+  P.wmax = wmax;
+  P.prev = prev;
+  for (int a = 0; a < 6; ++a) {
+    P.lo[a] = lo[a];
+    P.hi[a] = hi[a];
+  }
+  P.nv = nv;
+  Grid2 Gd;
+  Gd.gx = gx;
+  Gd.gy = gy;
+  Gd.x0 = lo[0];
+  Gd.y0 = lo[1];
+  Gd.hx = (hi[0] - lo[0]) / (double)gx;
+  Gd.hy = (hi[1] - lo[1]) / (double)gy;
+  hipLaunchKernelGGL(k_wrapped_grid2, dim3((unsigned)nblk), dim3(256), 0, st, P, T, Hd, base, Gd, iters, blk);
+  hipLaunchKernelGGL(k_wrapped_topk, dim3(1), dim3(1024), 0, st, blk, nblk, nbest, base, starts);
+  const long nstart = (long)nbest + nextra;
+  hipLaunchKernelGGL(k_wrapped_ms, dim3((unsigned)((nstart + 255) / 256)), dim3(256), 0, st, P, Hd, 0, starts,
+                     (int)nstart, iters, res);
+  hipLaunchKernelGGL(k_wrapped_best, dim3(1), dim3(1024), 0, st, res, nstart, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_wrapped_solve(hipStream_t st, const double* pos, const double* ang, long n, const double* y,
                                 double k, int mode, double w, double vmax, double wmax, const double* prev,
                                 const double* lo, const double* hi, int nv, int gn, const double* extra, int nextra,

@@ -56,7 +56,13 @@ SIGNATURES = {
     'rsl_preprocess_rows': (c_int, [_P, _P, c_longlong, c_int, _P, c_int, _P]),
     'rsl_phase_model': (c_int, [_P, _P, _P, c_longlong, _P, c_double, _P, c_int, c_double, _P, _P, _P]),
     'rsl_associate': (c_int, [_P, _P, c_int, _P, c_int, c_double, _P, _P, _P]),
+    'rsl_peak_topk': (c_int, [_P, _P, c_longlong, c_int, _P, _P, c_double, c_int, c_int, _P, _P, _P, _P]),
+    'rsl_associate_nearest': (c_int, [_P, _P, _P, _P, _P, c_int, c_longlong, c_double, _P, _P, _P]),
     'rsl_wrapped_scratch_bytes': (c_longlong, [c_longlong, c_int, c_int]),
+    'rsl_wrapped_search_scratch_bytes': (c_longlong, [c_longlong, POINTER(c_double), POINTER(c_double), c_double, c_int, c_int]),
+    'rsl_wrapped_search': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, c_double, c_double, _P,
+                                   POINTER(c_double), POINTER(c_double), c_int, POINTER(c_double), c_double, c_int, _P,
+                                   c_int, c_int, _P, c_longlong, _P]),
     'rsl_wrapped_solve': (c_int, [_P, _P, _P, c_longlong, _P, c_double, c_int, c_double, c_double, c_double, _P,
                                   POINTER(c_double), POINTER(c_double), c_int, c_int, _P, c_int, c_int, _P,
                                   c_longlong, _P]),

@@ -294,3 +294,46 @@ def wrapped_solve(pos, ang, y, k, *, mode: int, lo, hi, nv: int = 6, w: float = 
                                     int(iters), _ptr(scratch), nbytes, _ptr(out)), 'rsl_wrapped_solve')
     o = to_host(out)
     return o[:6].copy(), float(o[6])
+
+
+def wrapped_search(pos, ang, y, k, *, mode: int, lo, hi, nv: int = 6, w: float = 0.01, vmax: float = 50.0,
+                   wmax: float = 10.0, prev=None, extra=None, spacing_frac: float = 0.5, nbest: int = 64,
+                   iters: int = 12, ctx: Optional[Context] = None):
+    """Basin-resolving global minimisation of the wrapped-phase cost (rsl_wrapped_search): 2-D Gauss-Newton in
+    (v_x, v_y) from a grid whose spacing is spacing_frac of the wrap period 2 pi / k, then the nv-D refinement from the
+    nbest best basins and the extra starts.  Returns (x6, cost)."""
+    from ctypes import c_double
+    c = _ctx(ctx)
+    torch = c.torch
+    pos = np.ascontiguousarray(np.asarray(pos, np.float64).reshape(-1, 3))
+    ang = np.ascontiguousarray(np.asarray(ang, np.float64).reshape(-1, 2))
+    n = pos.shape[0]
+    ex = None if extra is None else np.ascontiguousarray(np.asarray(extra, np.float64).reshape(-1, 6))
+    nextra = 0 if ex is None else ex.shape[0]
+    lo6 = (c_double * 6)(*[float(v) for v in lo])
+    hi6 = (c_double * 6)(*[float(v) for v in hi])
+    # x[2..5] during the 2-D stage: the regulariser's optimum for them (0; with a previous motion, Advanced's temporal
+    # term w 0.1 |x - prev|^2 against 10 w v_z^2: v_z = prev_z / 101, w = prev_w)
+    base = np.zeros(6)
+    if prev is not None and mode == 1:
+        p = np.asarray(prev, np.float64).reshape(6)
+        base[2] = p[2] * 0.1 / 10.1
+        base[3:] = p[3:] if nv == 6 else 0.0
+    b6 = (c_double * 6)(*[float(v) for v in base])
+    # at least 64 points per axis (a smooth landscape when k is small, e.g. the pipeline's lambda = fc / c)
+    width = max(min(float(hi[0]) - float(lo[0]), float(hi[1]) - float(lo[1])), 1e-9)
+    spacing = min(float(spacing_frac) * 2 * math.pi / abs(float(k)), width / 64)
+    nbytes = int(c.lib.rsl_wrapped_search_scratch_bytes(n, lo6, hi6, spacing, int(nbest), nextra))
+    if nbytes < 0:
+        raise ValueError('rsl_wrapped_search_scratch_bytes: bad arguments')
+    scratch = c.empty(((nbytes + 7) // 8,), torch.float64)
+    dp, da, dy = c.to_dev(pos.reshape(-1)), c.to_dev(ang.reshape(-1)), c.to_dev(np.asarray(y, np.float64))
+    dprev = c.to_dev(np.asarray(prev, np.float64).reshape(6)) if prev is not None else None
+    dex = c.to_dev(ex.reshape(-1)) if nextra else None
+    out = c.empty((8,), torch.float64)
+    c._bind()
+    c.check(c.lib.rsl_wrapped_search(c.h, _ptr(dp), _ptr(da), n, _ptr(dy), float(k), int(mode), float(w), float(vmax),
+                                     float(wmax), _ptr(dprev), lo6, hi6, int(nv), b6, spacing, int(nbest), _ptr(dex),
+                                     nextra, int(iters), _ptr(scratch), nbytes, _ptr(out)), 'rsl_wrapped_search')
+    o = to_host(out)
+    return o[:6].copy(), float(o[6])

@@ -284,6 +284,37 @@ class Context:
                                            _ptr(steer['c128']), _ptr(steer['phase']), _ptr(conf)), 'rsl_confidence')
         return conf
 
+    # -- configs[3] per-frame pattern ------------------------------------------------------------
+    def peak_topk(self, entry_base, entry_cap: int, e_coord, e_pdb, *, thr_db: float, kmax: int, C: int):
+        """Per cube k: the first kmax peak entries by power_db descending (stable; robust_angle_estimation.py:362-369).
+        Returns (sel_entry, sel_frame, sel_rc) i32 [ncube * kmax] and sel_n i32 [ncube]."""
+        torch = self.torch
+        ncube = int(entry_base.shape[0]) - 1
+        n = max(ncube * int(kmax), 1)
+        se, sf, sr = (self.empty((n,), torch.int32) for _ in range(3))
+        sn = self.empty((max(ncube, 1),), torch.int32)
+        self._bind()
+        self.check(self.lib.rsl_peak_topk(self.h, _ptr(entry_base), int(entry_cap), ncube, _ptr(e_coord), _ptr(e_pdb),
+                                          float(thr_db), int(kmax), int(C), _ptr(se), _ptr(sf), _ptr(sr), _ptr(sn)),
+                   'rsl_peak_topk')
+        return se, sf, sr, sn
+
+    def associate_nearest(self, range_m, az_rad, s0, off, *, thr: float = 5.0):
+        """The analyser's association (radarscenes_complete_analysis.py:274-305) for every frame of a batch:
+        range_m, az_rad f64 [N], s0 c128 [N] (first signature components), off i64 [nframes + 1] (device).
+        Returns (match i32 [N] within the previous frame, -1 = none; dist f64 [N]; phase f64 [N])."""
+        torch = self.torch
+        nframes = int(off.shape[0]) - 1
+        N = int(range_m.shape[0])
+        match = self.empty((max(N, 1),), torch.int32)
+        dist = self.empty((max(N, 1),), torch.float64)
+        phase = self.empty((max(N, 1),), torch.float64)
+        self._bind()
+        self.check(self.lib.rsl_associate_nearest(self.h, _ptr(range_m), _ptr(az_rad), _ptr(s0), _ptr(off), nframes, N,
+                                                  float(thr), _ptr(match), _ptr(dist), _ptr(phase)),
+                   'rsl_associate_nearest')
+        return match, dist, phase
+
     # -- a25-a29 ---------------------------------------------------------------------------------
     def velocity(self, az, y, seg, *, k: float, ridge: float = 0.0, bounds=(-50.0, 50.0, -50.0, 50.0),
                  amask=None, want_resid=False, out=None, gidx=None, az_table=None, n=None):

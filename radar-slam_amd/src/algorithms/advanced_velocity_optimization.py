@@ -6,9 +6,10 @@ Drop-in for ``src/algorithms/advanced_velocity_optimization.py`` of the referenc
 
 The reference minimises the wrapped-phase cost plus piecewise penalties (:153-223) with several
 differential-evolution runs (seed 42; DE ignores the initial guess, so the runs are identical).  Here each run
-is ``rsl_wrapped_solve`` mode 1: projected Gauss-Newton from every point of a dense (v_x, v_y) grid over the
-adaptive bounds plus the run's initial guess, keeping the lowest cost (see velocity_solver_improved.py for
-the basin structure).  The penalties are evaluated on the device with the reference's exact formulas.
+is ``rsl_wrapped_search`` mode 1: projected Gauss-Newton in (v_x, v_y) from every point of a grid whose spacing is
+half the wrap period, over the adaptive bounds (every basin of the cost is entered), then the 6-D refinement of the
+best basins and the run's initial guess, keeping the lowest cost (see velocity_solver_improved.py for the basin
+structure).  The penalties are evaluated on the device with the reference's exact formulas.
 Parity contract: cost <= the reference's DE cost for the same associations, bounds and previous motion.
 """
 from __future__ import annotations
@@ -22,7 +23,12 @@ from rsl import ops
 
 logger = logging.getLogger(__name__)
 
-GRID_N = 512
+SPACING = 0.5  # stage-1 grid spacing of rsl_wrapped_search, as a fraction of the wrap period 2 pi / k
+
+
+def _grid_starts(lo, hi, k):
+    h = SPACING * 2 * np.pi / k
+    return int(max(1, np.ceil((hi[0] - lo[0]) / h)) * max(1, np.ceil((hi[1] - lo[1]) / h)))
 
 
 class AdvancedVelocityOptimizer:
@@ -150,11 +156,11 @@ class AdvancedVelocityOptimizer:
         lo = [b[0] for b in bounds]
         hi = [b[1] for b in bounds]
         try:
-            x, cost = ops.wrapped_solve(target_positions, target_angles, observed_phases, self._k(dt), mode=1,
-                                        lo=lo, hi=hi, nv=6, w=self.regularization_weight, vmax=self.max_velocity,
-                                        wmax=self.max_angular_velocity, prev=previous_motion,
-                                        extra=np.asarray(initial_guess, np.float64)[None], grid_n=GRID_N)
-            return {'success': True, 'motion_params': x, 'cost': cost, 'iterations': GRID_N * GRID_N,
+            x, cost = ops.wrapped_search(target_positions, target_angles, observed_phases, self._k(dt), mode=1,
+                                         lo=lo, hi=hi, nv=6, w=self.regularization_weight, vmax=self.max_velocity,
+                                         wmax=self.max_angular_velocity, prev=previous_motion,
+                                         extra=np.asarray(initial_guess, np.float64)[None], spacing_frac=SPACING)
+            return {'success': True, 'motion_params': x, 'cost': cost, 'iterations': _grid_starts(lo, hi, self._k(dt)),
                     'initial_guess': initial_guess}
         except Exception as e:  # the reference reports a failed run and continues (:400-408)
             return {'success': False, 'motion_params': initial_guess, 'cost': float('inf'), 'iterations': 0,

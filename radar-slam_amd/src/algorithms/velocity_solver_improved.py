@@ -8,11 +8,13 @@ Device work (librsl):
   target in order, the nearest unused previous target closer than ``association_threshold``, :104-126),
   one workgroup with a block-wide (distance, index) argmin per step;
 * ``cost_function`` / ``compute_phase_difference_model`` -> ``rsl_phase_model`` (wrapped residuals, ridge 0.01);
-* ``two_step_optimization`` -> ``rsl_wrapped_solve`` (mode 0).  The reference minimises the wrapped,
-  regularised cost (:223-266) with differential evolution (seed 42, :387-396 and :421-430).  That cost has one
-  basin per 2 pi / k of radial velocity (0.0195 m/s at 77 GHz, dt = 0.1 s), so DE's answer is one local
-  minimum among millions.  librsl runs projected Gauss-Newton from every point of a dense (v_x, v_y) grid over
-  the same box (plus the initial guess) and keeps the lowest cost.  Parity contract: cost <= the reference's
+* ``two_step_optimization`` -> ``rsl_wrapped_search`` then ``rsl_wrapped_solve`` (mode 0).  The reference minimises
+  the wrapped, regularised cost (:223-266) with differential evolution (seed 42, :387-396 and :421-430).  That cost
+  has one basin per 2 pi / k of radial velocity (0.0195 m/s at 77 GHz, dt = 0.1 s), so DE's answer is one local
+  minimum among millions.  Step 1 runs projected Gauss-Newton in (v_x, v_y) from every point of a grid with half the
+  wrap period as spacing over the same box (every basin is entered), refines the best basins and the initial guess
+  in 3-D and keeps the lowest cost; step 2 refines in 6-D from step 1's answer, the initial guess and a 512 x 512
+  start grid.  Parity contract: cost <= the reference's
   DE cost (tests/test_gpu_wrapped.py against tests/golden/golden_wrapped.npz).
 """
 from __future__ import annotations
@@ -28,7 +30,8 @@ logger = logging.getLogger(__name__)
 
 _TRANS_BOUNDS = [(-50, 50), (-50, 50), (-10, 10)]                           # velocity_solver_improved.py:383
 _FULL_BOUNDS = _TRANS_BOUNDS + [(-10, 10), (-10, 10), (-10, 10)]           # :417-418
-GRID_N = 512  # (v_x, v_y) start grid per solve: 262,144 Gauss-Newton descents
+GRID_N = 512  # step 2: (v_x, v_y) start grid of the 6-DoF refinement (262,144 Gauss-Newton descents) + step 1's answer
+SPACING = 0.5  # step 1: rsl_wrapped_search grid spacing as a fraction of the wrap period 2 pi / k
 
 
 def _opt_result(x, fun, nfev, method):
@@ -144,7 +147,8 @@ class ImprovedVelocitySolver:
         hi3 = [b[1] for b in tb] + [0, 0, 0]
         g0 = np.asarray(initial_guess, np.float64).reshape(6)
         logger.info("Step 1: Solving for translational velocity...")
-        x3, c3 = ops.wrapped_solve(pos, ang, observed, k, mode=0, lo=lo3, hi=hi3, nv=3, extra=g0[None], grid_n=GRID_N)
+        x3, c3 = ops.wrapped_search(pos, ang, observed, k, mode=0, lo=lo3, hi=hi3, nv=3, extra=g0[None],
+                                    spacing_frac=SPACING)
         logger.info(f"Step 1 result: v_trans = {x3[:3]}")
         logger.info("Step 2: Refining with full 6-DoF motion...")
         g1 = np.concatenate([x3[:3], [0, 0, 0]])
@@ -155,12 +159,14 @@ class ImprovedVelocitySolver:
         predicted, residuals = m['pred'], m['resid']
         rmse = np.sqrt(np.mean(residuals ** 2))
         max_residual = np.max(np.abs(residuals))
+        h = SPACING * 2 * np.pi / k
+        nfev1 = int(max(1, np.ceil((hi3[0] - lo3[0]) / h)) * max(1, np.ceil((hi3[1] - lo3[1]) / h)))
         nfev = GRID_N * GRID_N
         results = {'success': True, 'velocity': velocity_est, 'angular_velocity': angular_velocity_est,
                    'cost': c6, 'rmse': rmse, 'max_residual': max_residual, 'residuals': residuals,
                    'predicted_phases': predicted, 'observed_phases': observed,
                    'num_associations': len(target_associations),
-                   'step1_result': _opt_result(x3[:3], c3, nfev, 'rsl_wrapped_solve, 3 unknowns'),
+                   'step1_result': _opt_result(x3[:3], c3, nfev1, 'rsl_wrapped_search, 3 unknowns'),
                    'step2_result': _opt_result(x6, c6, nfev, 'rsl_wrapped_solve, 6 unknowns')}
         logger.info("Optimization complete:")
         logger.info(f"  Velocity: {velocity_est}")
