@@ -226,17 +226,21 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   bool sup = true;
   int group = 1;
   hipError_t e;
+  // packed range spectra between K1 and K2 (6 B per value; the per-bin exponents after the packed tiles, inside the
+  // c64-sized work buffer the caller provides)
+  unsigned char* wexp =
+      rsl::work_packed_supported(C, S) ? (unsigned char*)work + (size_t)F * A * C * S * 6 : nullptr;
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                              dc_removal, (float2*)work, &sup);
+                              dc_removal, (float2*)work, &sup, wexp);
   }
   if (int r = hip_check(h, e, "range_fft")) return r;
   {
     Scope sc(h, RSL_K_DOPPLER_FFT);
     e = rsl::launch_doppler_detect(h->stream, (const float2*)work, F, A, C, S, tC, (float2*)rds, thr_power, i_lo,
                                    i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
-                                   (float*)peak_pow, &sup, &group);
+                                   (float*)peak_pow, &sup, &group, wexp);
   }
   if (peak_pow_group) *peak_pow_group = group;
   return hip_check(h, e, "doppler_detect");

@@ -61,6 +61,61 @@ RSL_DEV void st8(float2* p, float2 x) {
   }
 }
 
+// Packed `work` (K1 -> K2 at S = 512, C = 128).  Per K1 tile (frame, antenna, 8-chirp block cb)
+// a 24 KiB block of 6 planes x 256 bin pairs x 16 B: planes 0-2 hold the even bin 2p of pair p, planes 3-5 the odd
+// bin 2p + 1, each bin's 8 rows x (re, im) as 16 fields of 24 bits (12 dwords, 3 x 16 B).  Every K1 store and every K2
+// load is a 16-B access: a K1 wave stores 1 KiB runs (lane = pair), a K2 lane loads the 3 chunks of one (bin, chirp
+// block) and a wave's loads cover whole 128-B lines (16 bins = 8 pairs of one plane, or the other plane).  Each bin of a
+// tile has its own exponent e (int8, after the planes: [tile][512 bins]); a field is n = rint(v 2^(22 - e)), |n| < 2^22,
+// stored offset-binary (the low 24 bits of the f32 1.5 2^23 + n), so the value's error is <= 2^(e - 23) = two fp32 ulps
+// of the bin's largest component, fp32-class for the RDS (1e-5 max-relative tolerance) and the peak decisions.
+// 6 B per value instead of 8: K1 + K2 move 14.1 instead of 16.8 MB per cfg2 frame.
+constexpr float kPkMagic = 12582912.0f;  // 1.5 * 2^23
+constexpr int kPkPlane = 4096;           // bytes per plane of one tile (256 pairs x 16 B)
+constexpr int kPkTile = 6 * kPkPlane;    // bytes per tile
+// frexp exponent of the largest |component| (abs bits), clamped so that both scale factors are normal floats
+RSL_DEV int pk_exp(unsigned mbits) {
+  const int e = (int)((mbits >> 23) & 0xFFu) - 126;
+  return e < -100 ? -100 : (e > 127 ? 127 : e);
+}
+RSL_DEV float pk_pow2(int k) { return __uint_as_float((unsigned)(127 + k) << 23); }
+// 16 fields (8 complex) -> 12 dwords: groups of 4 fields u0..u3 -> u0 | u1 << 24, u1 >> 8 | u2 << 16, u2 >> 16 | u3 << 8
+RSL_DEV void pk_pack16(const float (&f)[16], float s, uint4 (&o)[3]) {
+  unsigned u[16], d[12];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    // fma rounds v s to the nearest integer (|v s| < 2^22); the min keeps a value that rounds up to 2^22 in range
+    const unsigned b = min(__float_as_uint(fmaf(f[c], s, kPkMagic)), 0x4B7FFFFFu);
+    u[c] = b & 0xFFFFFFu;
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    d[3 * g] = u[4 * g] | (u[4 * g + 1] << 24);
+    d[3 * g + 1] = (u[4 * g + 1] >> 8) | (u[4 * g + 2] << 16);
+    d[3 * g + 2] = (u[4 * g + 2] >> 16) | (u[4 * g + 3] << 8);
+  }
+  o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+  o[2] = make_uint4(d[8], d[9], d[10], d[11]);
+}
+RSL_DEV void pk_unpack16(const uint4 (&w)[3], float s, float (&f)[16]) {
+  const unsigned d[12] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w,
+                          w[2].x, w[2].y, w[2].z, w[2].w};
+  const float off = -kPkMagic * s;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const unsigned u0 = d[3 * g] & 0xFFFFFFu;
+    const unsigned u1 = __builtin_amdgcn_alignbit(d[3 * g + 1], d[3 * g], 24) & 0xFFFFFFu;
+    const unsigned u2 = __builtin_amdgcn_alignbit(d[3 * g + 2], d[3 * g + 1], 16) & 0xFFFFFFu;
+    const unsigned u3 = d[3 * g + 2] >> 8;
+    // 0x4B000000 | u = 2^23 + u = 1.5 2^23 + n exactly; (that - 1.5 2^23) s in one rounding (exact: n s)
+    f[4 * g] = fmaf(__uint_as_float(0x4B000000u | u0), s, off);
+    f[4 * g + 1] = fmaf(__uint_as_float(0x4B000000u | u1), s, off);
+    f[4 * g + 2] = fmaf(__uint_as_float(0x4B000000u | u2), s, off);
+    f[4 * g + 3] = fmaf(__uint_as_float(0x4B000000u | u3), s, off);
+  }
+}
+
 // Grid of a persistent kernel: resident workgroups only (occupancy x CUs), at most ntile.
 static long resident_grid(const void* kern, size_t lds, long ntile) {
   int nb = 0, dev = 0, ncu = 256;
@@ -161,12 +216,16 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // are static, every later one comes from the XCD's dequeue head, claimed one tile ahead (the atomic returns during a
 // whole tile), so workgroups that start late (CUs held by a concurrent kernel) take fewer tiles (tools/dyn.sh: K1 alone
 // 1.499 vs 1.667 ms per 1000 cfg2 frames for the static walk, outputs bit-identical).  Without DYN (grids of fewer
-// than 8 workgroups) the walk is static.  DBG 1 (development builds only): no FFT (ablation, wrong results).
-template <int S, int CB, bool DYN, int DBG = 0>
+// than 8 workgroups) the walk is static.  DBG (development builds only; ablations with wrong results): 1 no FFT,
+// 2 no cube loads (constant tiles), 3 loads and LDS staging only (no FFT, no stores).
+// PK: packed `work` (S = 512, CB = 8: thread tid holds bin pair tid of all 8 rows; see pk_pack16).
+template <int S, int CB, bool DYN, int DBG = 0, bool PK = false>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
-                                                           float2* __restrict__ work, int slot) {
+                                                           float2* __restrict__ work, int slot,
+                                                           unsigned char* __restrict__ wexp) {
+  static_assert(!PK || (S / 2 == kThreads && CB == 8), "packed work: S = 512, 8-row tiles");
   constexpr int LD = lp_row(S);
   constexpr int H = S / 2;                 // float4 (2 complex) per row
   constexpr int PF = CB * H / kThreads;    // float4 per thread per tile
@@ -195,7 +254,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
       const int r = idx / H;
       // unconditional (clamped) load, rows past nrows zeroed at consumption (a select on the loaded value here
       // would wait for it)
-      nx[q] = ld16<true>(src4 + (r < nrows ? idx : 0));
+      if constexpr (DBG == 2)
+        nx[q] = make_float4((float)tid, (float)q, (float)r, 1.f);
+      else
+        nx[q] = ld16<true>(src4 + (r < nrows ? idx : 0));
     }
   };
   __shared__ long s_nn;
@@ -222,19 +284,54 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
     }
     __syncthreads();
     if (tn < hi) load(nx, tn);  // in flight during the FFT below
+    if constexpr (DBG == 3) {  // loads only: keep the staged tile live, skip the FFT and the stores
+      if (buf[tid * 2].x == 1.2345e30f) work[tid] = buf[tid * 2];
+      if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
+      __syncthreads();
+      return;
+    }
     if constexpr (DBG != 1) fft_rows<S, CB, kThreads, LD, true>(buf, tws, tid);
     if (dc) {
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
       __syncthreads();
     }
-    float4* dst4 = reinterpret_cast<float4*>(work + ((size_t)fa * C + cb * CB) * S);
+    if constexpr (PK) {
+      // bins 2 tid (f0) and 2 tid + 1 (f1) of the tile's 8 rows (C % 8 == 0: all rows present)
+      float f0[16], f1[16];
+      unsigned m0 = 0u, m1 = 0u;
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int idx = tid + q * kThreads;
-      const int r = idx / H, s2 = idx - r * H;
-      if (r < nrows) {
-        const float2 lo2 = buf[r * LD + lp(2 * s2)], hi2 = buf[r * LD + lp(2 * s2 + 1)];
-        st16<true>(dst4 + idx, make_float4(lo2.x, lo2.y, hi2.x, hi2.y));
+      for (int q = 0; q < 8; ++q) {
+        const float2 a = buf[q * LD + lp(2 * tid)], b = buf[q * LD + lp(2 * tid + 1)];
+        f0[2 * q] = a.x;
+        f0[2 * q + 1] = a.y;
+        f1[2 * q] = b.x;
+        f1[2 * q + 1] = b.y;
+        m0 = max(m0, max(__float_as_uint(a.x) & 0x7FFFFFFFu, __float_as_uint(a.y) & 0x7FFFFFFFu));
+        m1 = max(m1, max(__float_as_uint(b.x) & 0x7FFFFFFFu, __float_as_uint(b.y) & 0x7FFFFFFFu));
+      }
+      const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+      uint4 w0[3], w1[3];
+      pk_pack16(f0, pk_pow2(22 - e0), w0);
+      pk_pack16(f1, pk_pow2(22 - e1), w1);
+      const size_t tile = (size_t)fa * (C / CB) + cb;
+      uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile) + tid;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        st16<true>(reinterpret_cast<float4*>(dst + j * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[j]));
+        st16<true>(reinterpret_cast<float4*>(dst + (j + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[j]));
+      }
+      reinterpret_cast<unsigned short*>(wexp + tile * S)[tid] =
+          (unsigned short)((unsigned)(e0 & 0xFF) | ((unsigned)(e1 & 0xFF) << 8));
+    } else {
+      float4* dst4 = reinterpret_cast<float4*>(work + ((size_t)fa * C + cb * CB) * S);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int idx = tid + q * kThreads;
+        const int r = idx / H, s2 = idx - r * H;
+        if (r < nrows) {
+          const float2 lo2 = buf[r * LD + lp(2 * s2)], hi2 = buf[r * LD + lp(2 * s2 + 1)];
+          st16<true>(dst4 + idx, make_float4(lo2.x, lo2.y, hi2.x, hi2.y));
+        }
       }
     }
     if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
@@ -499,13 +596,17 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-template <int C, int KB, int NT, bool PAD, int DBG = 0>
+// PK: packed `work` (C = 128, KB = 16, NT = 256; see pk_pack16): thread (bin b, chirp block cb) = (tid & 15, tid >> 4)
+// loads its bin's 3 chunks of block cb (3 x 16 B) and the bin's exponent, decodes 8 chirps into its LDS row; threads
+// 0-31 do the same for the two halo bins.
+template <int C, int KB, int NT, bool PAD, int DBG = 0, bool PK = false>
 __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                        const float2* __restrict__ tw, float2* __restrict__ rds,
                                                        float thr_f, int i_lo, int i_hi,
                                                        unsigned long long* __restrict__ mask,
                                                        int* __restrict__ row_count, float* __restrict__ dbmap,
-                                                       float* __restrict__ pk_pow) {
+                                                       float* __restrict__ pk_pow,
+                                                       const unsigned char* __restrict__ wexp) {
   constexpr int NR = KB + 2;
   constexpr int LD = lp_rowp<PAD>(C) | 1;  // odd: conflict-free transposed (column) writes
   constexpr int PER = (NR * C + NT - 1) / NT;
@@ -531,13 +632,56 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   // (one address add per load, 128-B aligned row segments), then the two halo rows spread over all threads
   constexpr int CS = NT / KB;
   constexpr bool STRUCT = (NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16);
-  if constexpr (STRUCT) {
+  if constexpr (PK) {
+    static_assert(C == 128 && KB == 16 && NT == 256 && PAD, "packed work: C = 128, KB = 16, 256 threads");
+    constexpr int NCB = C / 8;
+    const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
+    const size_t tile0 = (size_t)fa * NCB;
+    // one (bin k, chirp block cbx) unit: 3 x 16 B from the bin's planes, and the bin's exponent
+    auto unit = [&](int k, int cbx, uint4(&w)[3], int& e) {
+      const uint4* src = reinterpret_cast<const uint4*>(wb + (tile0 + cbx) * kPkTile + (size_t)(3 * (k & 1)) * kPkPlane) +
+                         (k >> 1);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if constexpr (DBG == 6)
+          w[j] = make_uint4(0x4B4000u + tid, 0x5Au * j, 0x4B40u + k, 0x12345u);
+        else
+          w[j] = src[j * (kPkPlane / 16)];
+      }
+      e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cbx) * (size_t)S + k];
+    };
+    const int b = tid & 15, cb = tid >> 4;
+    uint4 wi[3], wh[3];
+    int ei, eh = 0;
+    unit(k0 + b, cb, wi, ei);
+    const bool halo = tid < 2 * NCB;  // threads 0-31: (side, chirp block) = (tid >> 4, tid & 15)
+    const int hside = tid >> 4, hcb = tid & 15;
+    if (halo) {
+      int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
+      kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+      unit(kk, hcb, wh, eh);
+    }
+#pragma unroll
+    for (int q = 0; q < TWP; ++q)
+      if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
+    float f[16];
+    pk_unpack16(wi, pk_pow2(ei - 22), f);
+    float2* row = buf + (b + 1) * LD + lpp<PAD>(8 * cb);  // 8 consecutive chirps: contiguous in the padded row
+#pragma unroll
+    for (int r = 0; r < 8; ++r) row[r] = make_float2(f[2 * r], f[2 * r + 1]);
+    if (halo) {
+      pk_unpack16(wh, pk_pow2(eh - 22), f);
+      float2* hrow = buf + (hside ? NR - 1 : 0) * LD + lpp<PAD>(8 * hcb);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) hrow[r] = make_float2(f[2 * r], f[2 * r + 1]);
+    }
+  } else if constexpr (STRUCT) {
     constexpr int PI = C / CS, PH = (2 * C + NT - 1) / NT;
     const int ri = tid % KB, cs = tid / KB;
     float2 ld[PI + PH];
     const float2* p = src + (unsigned)(cs * S + k0 + ri);
 #pragma unroll
-    for (int q = 0; q < PI; ++q) ld[q] = p[(unsigned)(q * CS * S)];
+    for (int q = 0; q < PI; ++q) ld[q] = DBG == 6 ? make_float2((float)tid, (float)q) : p[(unsigned)(q * CS * S)];
     int kl = k0 - 1, kh = k0 + KB;  // halo range bins (periodic: reflect is applied in the detect stage)
     if (kl < 0) kl += S;
     if (kh >= S) kh -= S;
@@ -546,7 +690,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
       const int e = tid + h * NT;
       if ((2 * C) % NT == 0 || e < 2 * C) {
         const int side = e / C, c = e - side * C;
-        ld[PI + h] = src[(unsigned)(c * S + (side ? kh : kl))];
+        ld[PI + h] = DBG == 6 ? make_float2((float)c, (float)h) : src[(unsigned)(c * S + (side ? kh : kl))];
       }
     }
 #pragma unroll
@@ -588,6 +732,10 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
     }
   }
   __syncthreads();
+  if constexpr (DBG == 7) {  // loads and LDS staging only
+    if (buf[tid].x == 1.2345e30f) rds[tid] = buf[tid];
+    return;
+  }
   if constexpr (PAD && (DBG == 0 || DBG >= 4) && dd_reg_ok<C, KB, NT>()) {
     fft_rows<C, NR, NT, LD, false, PAD>(buf, tws, tid);
     dd_tile_compute_reg<C, KB, NT, DBG>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi,
@@ -601,7 +749,8 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 template <int C, int KB>
 static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw,
                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                int* row_count, float* dbmap, float* pk_pow, int* pk_group) {
+                                int* row_count, float* dbmap, float* pk_pow, int* pk_group,
+                                const unsigned char* wexp) {
   constexpr int NT = 256;
   const long ntile = (long)F * A * (S / KB);
   // padded LDS rows (plain rows measured slower: 2.14 vs 1.98 ms per 1000 cfg2 frames) + the register body's exchange
@@ -611,6 +760,9 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // One tile per workgroup, 256 threads.  Measured and not kept: a persistent variant with a register prefetch of the
   // next tile (5.0-5.25 vs 3.85 ms per 2000 cfg2 frames), a 320-thread block (2.72 vs 2.48 ms per 1000 frames).
   auto kern = k_doppler_detect<C, KB, NT, true>;
+  if constexpr (C == 128 && KB == 16) {
+    if (wexp) kern = k_doppler_detect<C, KB, NT, true, 0, true>;  // packed work (work_packed_supported)
+  }
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
     const int v = atoi(e);
@@ -619,12 +771,21 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
     if (v == 3) kern = k_doppler_detect<C, KB, NT, true, 3>;
     if (v == 4) kern = k_doppler_detect<C, KB, NT, true, 4>;
     if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5>;
+    if (v == 6) kern = k_doppler_detect<C, KB, NT, true, 6>;
+    if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 7>;
+    if constexpr (C == 128 && KB == 16) {
+      if (wexp && v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, true>;
+      if (wexp && v == 4) kern = k_doppler_detect<C, KB, NT, true, 4, true>;
+      if (wexp && v == 5) kern = k_doppler_detect<C, KB, NT, true, 5, true>;
+      if (wexp && v == 6) kern = k_doppler_detect<C, KB, NT, true, 6, true>;
+      if (wexp && v == 7) kern = k_doppler_detect<C, KB, NT, true, 7, true>;
+    }
   }
 #endif
   // tile-compact peak powers from the register tile body (KB rows per group), row-compact from the general body
   *pk_group = dd_reg_ok<C, KB, NT>() ? KB : 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, tw, rds, thr_f, i_lo, i_hi, mask,
-                     row_count, dbmap, pk_pow);
+                     row_count, dbmap, pk_pow, wexp);
   return hipGetLastError();
 }
 
@@ -640,17 +801,19 @@ static int dd_kb(int C, int S) {
 template <int C>
 static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
                              double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
-                             float* pk_pow, int* pk_group) {
+                             float* pk_pow, int* pk_group, const unsigned char* wexp) {
   constexpr int K0 = rows_for(C);
   constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
   if (dd_kb(C, S) == K1)
-    return launch_k2d_kb<C, K1>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group);
-  return launch_k2d_kb<C, K0>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group);
+    return launch_k2d_kb<C, K1>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group,
+                                wexp);
+  return launch_k2d_kb<C, K0>(st, work, F, A, S, tw, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group,
+                              wexp);
 }
 
 template <int S>
 static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
-                            const float2* table, const float2* tw, int dc, float2* work) {
+                            const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
   constexpr int CB = rows_for(S);
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
     // 8 chirp rows per tile at S = 512: 16 rows (78 KiB LDS) is faster alone (1.53 vs 1.63 ms per 1000 cfg2 frames)
@@ -658,9 +821,18 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     const long ntile = (long)F * A * ((C + CB - 1) / CB);
     const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CB * lp_row(S));
     auto kern = k_range_fft_p<S, CB, true>;
+    if constexpr (S / 2 == kThreads && CB == 8) {
+      if (wexp) kern = k_range_fft_p<S, CB, true, 0, true>;  // packed work (work_packed_supported)
+    }
 #ifdef RSL_DEV_KNOBS
-    if (const char* e = getenv("RSL_RF_DBG"))  // ablation (development builds only; results are wrong)
-      if (atoi(e) == 1) kern = k_range_fft_p<S, CB, true, 1>;
+    if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
+      const int v = atoi(e);
+      if (v == 1) kern = wexp ? k_range_fft_p<S, CB, true, 1, S / 2 == kThreads && CB == 8>
+                              : k_range_fft_p<S, CB, true, 1>;
+      if (v == 2) kern = wexp ? k_range_fft_p<S, CB, true, 2, S / 2 == kThreads && CB == 8>
+                              : k_range_fft_p<S, CB, true, 2>;
+      if (v == 3) kern = k_range_fft_p<S, CB, true, 3>;
+    }
 #endif
     const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
     int slot = 0;
@@ -669,9 +841,12 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       slot = next_slot.fetch_add(1) % kRfSlots;
     } else {
       kern = k_range_fft_p<S, CB, false>;
+      if constexpr (S / 2 == kThreads && CB == 8) {
+        if (wexp) kern = k_range_fft_p<S, CB, false, 0, true>;
+      }
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
-                       work, slot);
+                       work, slot, wexp);
     return hipGetLastError();
   }
   const long nblk = (long)F * A * ((C + CB - 1) / CB);
@@ -774,6 +949,16 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
 #define RSL_FFT_SIZES(X) \
   X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048) X(4096) X(25) X(50) X(100) X(200) X(400) X(800) X(1600)
 
+// Packed `work` between K1 and K2 (pk_pack16): the K1 tile holds one bin pair per thread (S = 512) and the K2 tile
+// one (bin, 8-chirp block) per thread (C = 128, KB = 16).  Development builds: RSL_WORK_C64=1 keeps c64 rows (A/B).
+bool work_packed_supported(int C, int S) {
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_WORK_C64"))
+    if (atoi(e) != 0) return false;
+#endif
+  return S == 512 && C == 128 && doppler_detect_supported(C, S) && dd_kb(C, S) == 16;
+}
+
 bool doppler_detect_supported(int C, int S) {
   if (!fft_supported(C) || (C & (C - 1)) != 0 || C < 8 || C > 1024 || (S & 1)) return false;  // LDS <= 64 KiB
   const int KB = dd_kb(C, S);
@@ -782,14 +967,16 @@ bool doppler_detect_supported(int C, int S) {
 
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group) {
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group,
+                                 const unsigned char* wexp) {
   *pk_group = 1;
   *supported = doppler_detect_supported(C, S);
   if (!*supported || F <= 0 || A <= 0) return hipSuccess;
   switch (C) {
 #define CASE(n) \
   case n:       \
-    return launch_k2d<n>(st, work, F, A, S, tw_C, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group);
+    return launch_k2d<n>(st, work, F, A, S, tw_C, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group, \
+                          wexp);
     CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
 #undef CASE
     default:
@@ -799,13 +986,14 @@ hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int 
 }
 
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
-                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported) {
+                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
+                            unsigned char* wexp) {
   *supported = true;
   if (F <= 0 || A <= 0 || C <= 0) return hipSuccess;
   switch (S) {
 #define CASE(n) \
   case n:       \
-    return launch_k1<n>(st, cube, F, A, Ct, chirp0, C, table, tw_S, dc, work);
+    return launch_k1<n>(st, cube, F, A, Ct, chirp0, C, table, tw_S, dc, work, wexp);
     RSL_FFT_SIZES(CASE)
 #undef CASE
     default:

@@ -16,7 +16,8 @@ __device__ __forceinline__ long long list_count(const long long* dev, long long 
 // K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
 // cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
-                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported);
+                            const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
+                            unsigned char* wexp = nullptr);
 // K2: Doppler FFT (C points) + fftshift on both axes, transposed store.
 // work c64 [F, A, C, S] -> rds c64 [F, A, S, C]
 hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
@@ -28,7 +29,11 @@ bool doppler_detect_supported(int C, int S);
 float threshold_as_float(double thr);  // largest float t <= thr
 hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
-                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group);
+                                 int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group,
+                                 const unsigned char* wexp = nullptr);
+// wexp non-null (both launches): `work` holds packed rows (rsl_fft.hip pk_pack16: 6 B per value in 24 KiB tiles, the
+// int8 per-bin exponents at wexp = work + F A C S 6 bytes) -- only where work_packed_supported(C, S).
+bool work_packed_supported(int C, int S);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);

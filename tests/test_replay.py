@@ -263,7 +263,7 @@ def _sequence_frames(gold):
 
 def _dataset(tmp_path):
     import json
-    (tmp_path / 'data').mkdir()
+    (tmp_path / 'data').mkdir(exist_ok=True)
     for n in ('sensors.json', 'sequences.json'):
         (tmp_path / 'data' / n).write_text(json.dumps({}))
     return str(tmp_path)
