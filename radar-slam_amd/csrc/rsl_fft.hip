@@ -218,14 +218,13 @@ __global__ __launch_bounds__(kThreads) void k_range_fft(const float2* __restrict
 // 1.499 vs 1.667 ms per 1000 cfg2 frames for the static walk, outputs bit-identical).  Without DYN (grids of fewer
 // than 8 workgroups) the walk is static.  DBG (development builds only; ablations with wrong results): 1 no FFT,
 // 2 no cube loads (constant tiles), 3 loads and LDS staging only (no FFT, no stores).
-// PK: packed `work` (S = 512, CB = 8: thread tid holds bin pair tid of all 8 rows; see pk_pack16).
-template <int S, int CB, bool DYN, int DBG = 0, bool PK = false>
+template <int S, int CB, bool DYN, int DBG = 0>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
                                                            float2* __restrict__ work, int slot,
                                                            unsigned char* __restrict__ wexp) {
-  static_assert(!PK || (S / 2 == kThreads && CB == 8), "packed work: S = 512, 8-row tiles");
+  (void)wexp;
   constexpr int LD = lp_row(S);
   constexpr int H = S / 2;                 // float4 (2 complex) per row
   constexpr int PF = CB * H / kThreads;    // float4 per thread per tile
@@ -295,43 +294,14 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
       if (tid < CB) buf[tid * LD] = make_float2(0.f, 0.f);
       __syncthreads();
     }
-    if constexpr (PK) {
-      // bins 2 tid (f0) and 2 tid + 1 (f1) of the tile's 8 rows (C % 8 == 0: all rows present)
-      float f0[16], f1[16];
-      unsigned m0 = 0u, m1 = 0u;
+    float4* dst4 = reinterpret_cast<float4*>(work + ((size_t)fa * C + cb * CB) * S);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float2 a = buf[q * LD + lp(2 * tid)], b = buf[q * LD + lp(2 * tid + 1)];
-        f0[2 * q] = a.x;
-        f0[2 * q + 1] = a.y;
-        f1[2 * q] = b.x;
-        f1[2 * q + 1] = b.y;
-        m0 = max(m0, max(__float_as_uint(a.x) & 0x7FFFFFFFu, __float_as_uint(a.y) & 0x7FFFFFFFu));
-        m1 = max(m1, max(__float_as_uint(b.x) & 0x7FFFFFFFu, __float_as_uint(b.y) & 0x7FFFFFFFu));
-      }
-      const int e0 = pk_exp(m0), e1 = pk_exp(m1);
-      uint4 w0[3], w1[3];
-      pk_pack16(f0, pk_pow2(22 - e0), w0);
-      pk_pack16(f1, pk_pow2(22 - e1), w1);
-      const size_t tile = (size_t)fa * (C / CB) + cb;
-      uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile) + tid;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        st16<true>(reinterpret_cast<float4*>(dst + j * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[j]));
-        st16<true>(reinterpret_cast<float4*>(dst + (j + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[j]));
-      }
-      reinterpret_cast<unsigned short*>(wexp + tile * S)[tid] =
-          (unsigned short)((unsigned)(e0 & 0xFF) | ((unsigned)(e1 & 0xFF) << 8));
-    } else {
-      float4* dst4 = reinterpret_cast<float4*>(work + ((size_t)fa * C + cb * CB) * S);
-#pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        const int idx = tid + q * kThreads;
-        const int r = idx / H, s2 = idx - r * H;
-        if (r < nrows) {
-          const float2 lo2 = buf[r * LD + lp(2 * s2)], hi2 = buf[r * LD + lp(2 * s2 + 1)];
-          st16<true>(dst4 + idx, make_float4(lo2.x, lo2.y, hi2.x, hi2.y));
-        }
+    for (int q = 0; q < PF; ++q) {
+      const int idx = tid + q * kThreads;
+      const int r = idx / H, s2 = idx - r * H;
+      if (r < nrows) {
+        const float2 lo2 = buf[r * LD + lp(2 * s2)], hi2 = buf[r * LD + lp(2 * s2 + 1)];
+        st16<true>(dst4 + idx, make_float4(lo2.x, lo2.y, hi2.x, hi2.y));
       }
     }
     if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
@@ -355,6 +325,170 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
   }
   long t = blockIdx.x;
   float4 nx[PF];
+  if (t < ntile) load(nx, t);
+  for (; t < ntile; t += G) body(nx, t, t + G);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 for S = 512 with packed `work` (the cfg2 shape): the range FFT as 16 x 32 in registers instead of three radix-8
+// Stockham passes through LDS.  The LDS FFT was LDS-bound (SQ_LDS_IDX_ACTIVE ~70 % of the kernel's cycles, 21 % of wave
+// time waiting on LDS issue, 42 % extra bank-conflict cycles): staging + 3 stage writes + 3 stage reads + the output
+// read.  Here a tile (8 chirp rows of one (frame, antenna)) takes two LDS exchanges, both conflict-free:
+//   a tile is chirp class c of one (frame, antenna): the 8 chirps c + 16 q (q < 8; C = 128, c < 16), so that K2's
+//   Doppler transform can start with a radix-8 step in registers (k_doppler_detect_r128);
+//   x[n], n = j + 32 m (j < 32, m < 16), thread t = (row q = t / 32, j = t % 32) loads x[j + 32 m] of chirp c + 16 q
+//   (8-B loads, two 256-B runs per wave instruction) and multiplies by conj(ref) w;
+//   stage 1: V[j][k1] = DFT16_m x[j + 32 m]  (registers), times W512^(j k1) (LDS table, 17-float2 pitch per j);
+//   exchange: V' -> xbuf[row][k1][j] (pitch 34: the stage-2 reads of 32 lanes hit 64 distinct banks);
+//   stage 2: thread t = (row, k1 = (t / 2) % 16, h = t % 2) takes j = 2 i + h: E or O = DFT16_i (registers); lane
+//   pairs swap halves by DPP and form X[k1 + 16 k2] = E + W32^k2 O, X[k1 + 16 (k2 + 16)] = E - W32^k2 O;
+//   output: X -> obuf[row][b + 8 (b / 256)] (the b >= 256 half shifted by 8: conflict-free writes), then thread p
+//   reads bins 2p, 2p + 1 of the 8 rows (16-B reads) and stores them packed (pk_pack16).
+// X[k1 + 16 k2'] = sum_j W512^(j k1) W32^(j k2') sum_m x[j + 32 m] W16^(m k1): the 512-point DFT exactly.
+// DBG (development builds only; wrong results): 2 no cube loads, 3 loads only.
+constexpr int kR512Pitch = 34;             // xbuf pitch per (row, k1): 32 j + 2 pad
+constexpr int kR512Obuf = 520;             // obuf row pitch (512 bins + 8 shift)
+constexpr int kR512TwPitch = 17;           // ldtw pitch per j
+RSL_DEV float2 w32(int k) {                // exp(-2 pi i k / 32), k < 16
+  constexpr float c[16] = {1.f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f,
+                           0.70710678118654757f, 0.55557023301960229f, 0.38268343236508984f, 0.19509032201612833f,
+                           0.f, -0.19509032201612819f, -0.38268343236508973f, -0.55557023301960196f,
+                           -0.70710678118654746f, -0.83146961230254535f, -0.92387953251128674f, -0.98078528040323043f};
+  return make_float2(c[k], c[(k + 8) & 15] * (k < 8 ? 1.f : -1.f));  // -sin(2 pi k / 32)
+}
+
+template <bool DYN, int DBG = 0>
+__global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __restrict__ cube, int A, int Ct, int c0,
+                                                              int C, long ntile, const float2* __restrict__ table,
+                                                              const float2* __restrict__ tw, int dc,
+                                                              float2* __restrict__ work, int slot,
+                                                              unsigned char* __restrict__ wexp) {
+  constexpr int S = 512, CB = 8;
+  __shared__ float2 ldtab[S];
+  __shared__ float2 ldtw[32 * kR512TwPitch];
+  __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // stage exchange; aliased by the output buffer
+  static_assert(CB * kR512Obuf <= CB * 16 * kR512Pitch, "output buffer must fit in the exchange buffer");
+  float2* obuf = xbuf;
+  const int tid = threadIdx.x;
+  const int row = tid >> 5, j = tid & 31;
+  const int k1b = (tid >> 1) & 15, h = tid & 1;
+  const int ncb = C / CB;
+  const long G = gridDim.x;
+  for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
+  for (int k = tid; k < 32 * 16; k += kThreads) {
+    const int jj = k >> 4, kk = k & 15;
+    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
+  }
+  auto load = [&](float2(&nx)[16], long t) {
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 16 * row) * S + j;  // chirp class cb, row q = row
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if constexpr (DBG == 2)
+        nx[m] = make_float2((float)tid, (float)m);
+      else
+        nx[m] = ld8<true>(src + 32 * m);
+    }
+  };
+  __shared__ long s_nn;
+  const int xcd = blockIdx.x & 7;
+  const long gx = (G - xcd + 7) / 8;
+  const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
+  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  __syncthreads();
+  auto body = [&](float2(&nx)[16], long t, long tn) {
+    unsigned claim = 0;
+    if (DYN && tid == 0) claim = atomicAdd(head, 1u);
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 32 * m]);
+    if (tn < hi) load(nx, tn);  // in flight during this tile's transforms and stores
+    if constexpr (DBG == 3) {
+      if (v[0].x == 1.2345e30f) work[tid] = v[1];
+      if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
+      __syncthreads();
+      return;
+    }
+    // stage 1: DFT16 over m, twiddle W512^(j k1)
+    Dft<16>::run(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[j * kR512TwPitch + k]);
+    float2* xw = xbuf + row * 16 * kR512Pitch + j;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xw[k * kR512Pitch] = v[k];
+    __syncthreads();
+    // stage 2: DFT16 over i of V'[2 i + h][k1], then the radix-2 combine across the lane pair (h = 0, 1)
+    const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
+    Dft<16>::run(v);
+    float2 xo[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float2 t2 = cmul(v[k], w32(k));  // W32^k O[k] (used by the h = 1 lane)
+      const float2 send = h ? t2 : v[k];
+      float2 recv;
+      recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, true));
+      recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, true));
+      const float2 a = h ? recv : v[k], b = h ? t2 : recv;  // a = E[k], b = W32^k O[k]
+      xo[k] = h ? csub(a, b) : cadd(a, b);                    // bin k1 + 16 (k + 16 h)
+    }
+    if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
+    __syncthreads();  // xbuf reads done: obuf aliases it
+    float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;  // bin k1 + 16 k + 256 h at position bin + 8 h
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ow[16 * k] = xo[k];
+    __syncthreads();
+    // packed store: thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows
+    float f0[16], f1[16];
+    unsigned m0 = 0u, m1 = 0u;
+    const int pos = 2 * tid + (tid >= 128 ? 8 : 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * kR512Obuf + pos);
+      f0[2 * q] = ab.x;
+      f0[2 * q + 1] = ab.y;
+      f1[2 * q] = ab.z;
+      f1[2 * q + 1] = ab.w;
+      m0 = max(m0, max(__float_as_uint(ab.x) & 0x7FFFFFFFu, __float_as_uint(ab.y) & 0x7FFFFFFFu));
+      m1 = max(m1, max(__float_as_uint(ab.z) & 0x7FFFFFFFu, __float_as_uint(ab.w) & 0x7FFFFFFFu));
+    }
+    const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+    uint4 w0[3], w1[3];
+    pk_pack16(f0, pk_pow2(22 - e0), w0);
+    pk_pack16(f1, pk_pow2(22 - e1), w1);
+    const size_t tile = (size_t)fa * ncb + cb;
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile) + tid;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
+      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
+    }
+    reinterpret_cast<unsigned short*>(wexp + tile * S)[tid] =
+        (unsigned short)((unsigned)(e0 & 0xFF) | ((unsigned)(e1 & 0xFF) << 8));
+    if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
+    __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
+  };
+  if constexpr (DYN) {
+    long t = lo + (blockIdx.x >> 3), tn = t + gx;
+    float2 nx[16];
+    if (t < hi) load(nx, t);
+    while (t < hi) {
+      body(nx, t, tn);
+      t = tn;
+      tn = s_nn;
+    }
+    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+      atomicExch(head, 0u);
+      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+    }
+    return;
+  }
+  long t = blockIdx.x;
+  float2 nx[16];
   if (t < ntile) load(nx, t);
   for (; t < ntile; t += G) body(nx, t, t + G);
 }
@@ -487,7 +621,8 @@ constexpr bool dd_reg_ok() {
 // lane-pair DPP swap measured slower, 1.698 vs 1.677 ms per 1000 cfg2 frames); neighbour lanes and the peak-offset scan
 // use DPP (wave_shr / wave_shl, row_shr / row_bcast: K2 3.52 vs 3.76 ms per 2000 cfg2 frames against ds_bpermute);
 // the tile's compacted peak powers are staged in the dead LDS tile and stored block-wide (tools/pkb.sh).
-// DBG (development builds only, ablations with wrong results): 4 no peak-power stores, 5 no mask / count stores.
+// DBG (development builds only, ablations with wrong results): 4 no peak-power stores, 5 no mask / count stores,
+// 8 no RDS stores, 9 RDS stores only (no detection).
 template <int C, int KB, int NT, int DBG = 0>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
@@ -511,7 +646,11 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   for (int r = 0; r < 10; ++r) {
     const float2 z = col[(rb + r) * LD];
     p[r] = cabs2(z);
-    if (r >= 1 && r <= 8) st8<true>(dst + (size_t)(r - 1) * C, z);
+    if (DBG != 8 && r >= 1 && r <= 8) st8<true>(dst + (size_t)(r - 1) * C, z);  // DBG 8: no RDS stores
+  }
+  if constexpr (DBG == 9) {  // DBG 9: RDS stores only, no detection
+    if (p[0] == 1.2345e30f) mask[tid] = 0ull;
+    return;
   }
   float vm[8];
 #pragma unroll
@@ -596,10 +735,7 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
 // shifted edges i = 0 / S-1, where 'reflect' means "no neighbour".  Saves k_detect's full RDS re-read.
 // Requires S % KB == 0 and (S/2) % KB == 0 (each block's shifted rows contiguous).
 // ---------------------------------------------------------------------------------------------
-// PK: packed `work` (C = 128, KB = 16, NT = 256; see pk_pack16): thread (bin b, chirp block cb) = (tid & 15, tid >> 4)
-// loads its bin's 3 chunks of block cb (3 x 16 B) and the bin's exponent, decodes 8 chirps into its LDS row; threads
-// 0-31 do the same for the two halo bins.
-template <int C, int KB, int NT, bool PAD, int DBG = 0, bool PK = false>
+template <int C, int KB, int NT, bool PAD, int DBG = 0>
 __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict__ work, int S,
                                                        const float2* __restrict__ tw, float2* __restrict__ rds,
                                                        float thr_f, int i_lo, int i_hi,
@@ -632,50 +768,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   // (one address add per load, 128-B aligned row segments), then the two halo rows spread over all threads
   constexpr int CS = NT / KB;
   constexpr bool STRUCT = (NT % KB == 0) && (C % (NT / KB) == 0) && ((NT / KB) % 8 == 0) && (C / (NT / KB) <= 16);
-  if constexpr (PK) {
-    static_assert(C == 128 && KB == 16 && NT == 256 && PAD, "packed work: C = 128, KB = 16, 256 threads");
-    constexpr int NCB = C / 8;
-    const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
-    const size_t tile0 = (size_t)fa * NCB;
-    // one (bin k, chirp block cbx) unit: 3 x 16 B from the bin's planes, and the bin's exponent
-    auto unit = [&](int k, int cbx, uint4(&w)[3], int& e) {
-      const uint4* src = reinterpret_cast<const uint4*>(wb + (tile0 + cbx) * kPkTile + (size_t)(3 * (k & 1)) * kPkPlane) +
-                         (k >> 1);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if constexpr (DBG == 6)
-          w[j] = make_uint4(0x4B4000u + tid, 0x5Au * j, 0x4B40u + k, 0x12345u);
-        else
-          w[j] = src[j * (kPkPlane / 16)];
-      }
-      e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cbx) * (size_t)S + k];
-    };
-    const int b = tid & 15, cb = tid >> 4;
-    uint4 wi[3], wh[3];
-    int ei, eh = 0;
-    unit(k0 + b, cb, wi, ei);
-    const bool halo = tid < 2 * NCB;  // threads 0-31: (side, chirp block) = (tid >> 4, tid & 15)
-    const int hside = tid >> 4, hcb = tid & 15;
-    if (halo) {
-      int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
-      kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
-      unit(kk, hcb, wh, eh);
-    }
-#pragma unroll
-    for (int q = 0; q < TWP; ++q)
-      if (C % NT == 0 || tid + q * NT < C) tws[tid + q * NT] = twv[q];
-    float f[16];
-    pk_unpack16(wi, pk_pow2(ei - 22), f);
-    float2* row = buf + (b + 1) * LD + lpp<PAD>(8 * cb);  // 8 consecutive chirps: contiguous in the padded row
-#pragma unroll
-    for (int r = 0; r < 8; ++r) row[r] = make_float2(f[2 * r], f[2 * r + 1]);
-    if (halo) {
-      pk_unpack16(wh, pk_pow2(eh - 22), f);
-      float2* hrow = buf + (hside ? NR - 1 : 0) * LD + lpp<PAD>(8 * hcb);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) hrow[r] = make_float2(f[2 * r], f[2 * r + 1]);
-    }
-  } else if constexpr (STRUCT) {
+  if constexpr (STRUCT) {
     constexpr int PI = C / CS, PH = (2 * C + NT - 1) / NT;
     const int ri = tid % KB, cs = tid / KB;
     float2 ld[PI + PH];
@@ -746,6 +839,107 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
   }
 }
 
+// K2 + K3 for C = 128 with packed `work` (the cfg2 shape): the Doppler FFT as 8 x 16 in registers.  K1 stores chirp
+// class c (chirps c + 16 r, r < 8) as one packed tile, so thread (bin b, class c) = (tid % 16, tid / 16) loads the 8
+// chirps x[c + 16 r] of its bin (3 x 16 B) and
+//   stage 1: Y_c[k1] = DFT8_r x[c + 16 r] (registers), times W128^(c k1) (the twiddle table in LDS, broadcast reads);
+//   exchange: Y' -> xb[c][k1][b2] (b2 = LDS row: b + 1, halo rows 0 and 17 from threads 0-31), 144 float2 per class;
+//   stage 2: thread t < 144 = (k1 = t / 18, b2 = t % 18) reads xb[c][t] for c < 16 (consecutive per instruction),
+//   X[k1 + 8 k2] = DFT16_c (registers), written to the tile row b2 at the unshifted Doppler position;
+// then the register-form detection (dd_tile_compute_reg) as in k_doppler_detect.  X[k1 + 8 k2] = sum_c W128^(c k1)
+// W16^(c k2) sum_r x[c + 16 r] W8^(r k1): the 128-point DFT exactly.  Against the LDS Stockham form (staging + two
+// stage passes) a third less LDS traffic.  DBG (development builds only): 6 no work loads, 7 loads only.
+template <int DBG = 0>
+__global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __restrict__ work, int S,
+                                                            const float2* __restrict__ tw, float2* __restrict__ rds,
+                                                            float thr_f, int i_lo, int i_hi,
+                                                            unsigned long long* __restrict__ mask,
+                                                            int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                            float* __restrict__ pk_pow,
+                                                            const unsigned char* __restrict__ wexp) {
+  constexpr int C = 128, KB = 16, NT = 256, NR = KB + 2, NCB = 16;
+  constexpr int LD = lp_row(C) | 1;
+  constexpr int XP = 8 * NR;  // xb floats2 per class
+  static_assert(NCB * XP <= NR * LD, "exchange buffer must fit in the tile buffer");
+  extern __shared__ float2 sm[];
+  float2* tws = sm;
+  float2* buf = sm + C;
+  float2* xb = buf;  // exchange, then the tile rows (aliased: a barrier separates the last read from the first write)
+  const int tid = threadIdx.x;
+  const unsigned nkb = (unsigned)(S / KB);
+  const unsigned tile = (unsigned)xcd_tile(blockIdx.x, gridDim.x);
+  const int kb = (int)(tile % nkb);
+  const unsigned fa = tile / nkb;
+  const int k0 = kb * KB;
+  const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
+  const size_t tile0 = (size_t)fa * NCB;
+  auto unit = [&](int k, int cls, uint4(&w)[3], int& e) {
+    const uint4* src =
+        reinterpret_cast<const uint4*>(wb + (tile0 + cls) * kPkTile + (size_t)(3 * (k & 1)) * kPkPlane) + (k >> 1);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      if constexpr (DBG == 6)
+        w[jj] = make_uint4(0x4B4000u + tid, 0x5Au * jj, 0x4B40u + k, 0x12345u);
+      else
+        w[jj] = src[jj * (kPkPlane / 16)];
+    }
+    e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cls) * (size_t)S + k];
+  };
+  const float2 twv = tw[tid & (C - 1)];
+  const int b = tid & 15, cls = tid >> 4;
+  uint4 wi[3], wh[3];
+  int ei, eh = 0;
+  unit(k0 + b, cls, wi, ei);
+  const bool halo = tid < 2 * NCB;  // threads 0-31: (side, class) = (tid / 16, tid % 16)
+  const int hside = tid >> 4, hcls = tid & 15;
+  if (halo) {
+    int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
+    kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+    unit(kk, hcls, wh, eh);
+  }
+  if (tid < C) tws[tid] = twv;
+  __syncthreads();  // twiddles
+  if constexpr (DBG == 7) {
+    if (__uint_as_float(wi[0].x ^ wh[1].y) == 1.2345e30f) rds[tid] = make_float2((float)ei, (float)eh);
+    return;
+  }
+  // stage 1 for one unit: decode, DFT8 over r, twiddle W128^(c k1), write xb[c][k1][b2]
+  auto stage1 = [&](const uint4(&w)[3], int e, int c, int b2) {
+    float f[16];
+    pk_unpack16(w, pk_pow2(e - 22), f);
+    float2 y[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) y[r] = make_float2(f[2 * r], f[2 * r + 1]);
+    Dft<8>::run(y);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) y[k] = cmul(y[k], tws[c * k]);
+    float2* dst = xb + c * XP + b2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[k * NR] = y[k];
+  };
+  stage1(wi, ei, cls, b + 1);
+  if (halo) stage1(wh, eh, hcls, hside ? NR - 1 : 0);
+  __syncthreads();
+  // stage 2: DFT16 over the classes
+  float2 x[16];
+  const bool s2 = tid < XP;
+  const int k1 = tid / NR, b2 = tid - (tid / NR) * NR;
+  if (s2) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = xb[c * XP + tid];
+    Dft<16>::run(x);
+  }
+  __syncthreads();  // xb reads done: the tile rows alias it
+  if (s2) {
+    float2* row = buf + b2 * LD;
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) row[lp(k1 + 8 * k2)] = x[k2];
+  }
+  __syncthreads();
+  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0>(
+      buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+}
+
 template <int C, int KB>
 static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw,
                                 float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
@@ -761,7 +955,7 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // next tile (5.0-5.25 vs 3.85 ms per 2000 cfg2 frames), a 320-thread block (2.72 vs 2.48 ms per 1000 frames).
   auto kern = k_doppler_detect<C, KB, NT, true>;
   if constexpr (C == 128 && KB == 16) {
-    if (wexp) kern = k_doppler_detect<C, KB, NT, true, 0, true>;  // packed work (work_packed_supported)
+    if (wexp) kern = k_doppler_detect_r128<>;  // packed work (work_packed_supported): register-form transform
   }
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
@@ -774,11 +968,12 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
     if (v == 6) kern = k_doppler_detect<C, KB, NT, true, 6>;
     if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 7>;
     if constexpr (C == 128 && KB == 16) {
-      if (wexp && v == 1) kern = k_doppler_detect<C, KB, NT, true, 1, true>;
-      if (wexp && v == 4) kern = k_doppler_detect<C, KB, NT, true, 4, true>;
-      if (wexp && v == 5) kern = k_doppler_detect<C, KB, NT, true, 5, true>;
-      if (wexp && v == 6) kern = k_doppler_detect<C, KB, NT, true, 6, true>;
-      if (wexp && v == 7) kern = k_doppler_detect<C, KB, NT, true, 7, true>;
+      if (wexp && v == 4) kern = k_doppler_detect_r128<4>;
+      if (wexp && v == 5) kern = k_doppler_detect_r128<5>;
+      if (wexp && v == 6) kern = k_doppler_detect_r128<6>;
+      if (wexp && v == 7) kern = k_doppler_detect_r128<7>;
+      if (wexp && v == 8) kern = k_doppler_detect_r128<8>;
+      if (wexp && v == 9) kern = k_doppler_detect_r128<9>;
     }
   }
 #endif
@@ -821,32 +1016,38 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     const long ntile = (long)F * A * ((C + CB - 1) / CB);
     const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CB * lp_row(S));
     auto kern = k_range_fft_p<S, CB, true>;
-    if constexpr (S / 2 == kThreads && CB == 8) {
-      if (wexp) kern = k_range_fft_p<S, CB, true, 0, true>;  // packed work (work_packed_supported)
+    size_t lds_k = lds;
+    if constexpr (S == 512 && CB == 8) {
+      if (wexp) {  // packed work (work_packed_supported): the register-form 16 x 32 transform
+        kern = k_range_fft_r512<true>;
+        lds_k = 0;  // static LDS only
+      }
     }
 #ifdef RSL_DEV_KNOBS
     if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
       const int v = atoi(e);
-      if (v == 1) kern = wexp ? k_range_fft_p<S, CB, true, 1, S / 2 == kThreads && CB == 8>
-                              : k_range_fft_p<S, CB, true, 1>;
-      if (v == 2) kern = wexp ? k_range_fft_p<S, CB, true, 2, S / 2 == kThreads && CB == 8>
-                              : k_range_fft_p<S, CB, true, 2>;
-      if (v == 3) kern = k_range_fft_p<S, CB, true, 3>;
+      if constexpr (S == 512 && CB == 8) {
+        if (wexp && v == 2) kern = k_range_fft_r512<true, 2>;
+        if (wexp && v == 3) kern = k_range_fft_r512<true, 3>;
+      }
+      if (!wexp && v == 1) kern = k_range_fft_p<S, CB, true, 1>;
+      if (!wexp && v == 2) kern = k_range_fft_p<S, CB, true, 2>;
+      if (!wexp && v == 3) kern = k_range_fft_p<S, CB, true, 3>;
     }
 #endif
-    const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds, ntile);
+    const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds_k, ntile);
     int slot = 0;
     if (nblk >= 8) {  // the per-XCD dequeue needs a workgroup on every XCD
       static std::atomic<int> next_slot{0};
       slot = next_slot.fetch_add(1) % kRfSlots;
     } else {
       kern = k_range_fft_p<S, CB, false>;
-      if constexpr (S / 2 == kThreads && CB == 8) {
-        if (wexp) kern = k_range_fft_p<S, CB, false, 0, true>;
+      if constexpr (S == 512 && CB == 8) {
+        if (wexp) kern = k_range_fft_r512<false>;
       }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
-                       work, slot, wexp);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds_k, st, cube, A, Ct, c0, C, ntile, table, tw,
+                       dc, work, slot, wexp);
     return hipGetLastError();
   }
   const long nblk = (long)F * A * ((C + CB - 1) / CB);

@@ -1,7 +1,8 @@
 """K1 / K2 ablations on one cfg2 batch, c64 and packed `work` (development library, RSL_LIBRARY=librsl_dev.so):
 the standalone time of each kernel with one part removed (results are wrong in the variants; only times matter).
   RSL_RF_DBG: 1 no FFT, 2 no cube loads, 3 loads + LDS staging only
-  RSL_DD_DBG: 1 no FFT, 4 no peak-power stores, 5 no mask stores, 6 no work loads, 7 loads + LDS staging only
+  RSL_DD_DBG: 1 no FFT, 4 no peak-power stores, 5 no mask stores, 6 no work loads, 7 loads + LDS staging only,
+              8 no RDS stores, 9 RDS stores only (no detection) -- 8 and 9 in the packed (register-form) kernel only
 RSL_WORK_C64=1 keeps c64 rows.  GPU box:  RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so python tools/fft_ablation.py"""
 import os
 import sys
@@ -42,10 +43,10 @@ def timed(env):
 
 
 variants = []
-for c64 in ('1', '0'):
+for c64 in (os.environ.get('C64', '1,0')).split(','):
     for rf in ('0', '1', '2', '3'):
         variants.append(('K1', {'RSL_WORK_C64': c64, 'RSL_RF_DBG': rf}))
-    for dd in ('0', '1', '4', '5', '6', '7'):
+    for dd in ('0', '1', '4', '5', '6', '7') + (('8', '9') if c64 == '0' else ()):
         variants.append(('K2', {'RSL_WORK_C64': c64, 'RSL_DD_DBG': dd}))
 best = {}
 for rep in range(3):
