@@ -30,16 +30,19 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
 DIST = False  # a torch.distributed process group is up (set in main)
-PROFILE = os.path.join(ROOT, 'profiles', 'r2o_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r3a_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
+TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
+                  ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')
 
 
 def pmc_traffic(kernel_prefix, frames_per_launch, config='cfg2'):
     """HBM bytes per launch of a kernel from the committed PMC profile (FETCH_SIZE x 2 + WRITE_SIZE, per
-    MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present or the profile was
-    collected on another workload."""
+    MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present, the profile was
+    collected on another workload or holds no kernel of that name (a kernel renamed or replaced since: the profile is
+    stale for it, and its bytes are not reported)."""
     if config != PROFILE_CONFIG:
         return None
     try:
@@ -65,40 +68,51 @@ def make_cubes(ctx, nb, F, A, C, Tc, rank):
 
 
 def _cpu_frame(args):
-    """Work item of cpu_baseline's process pool, on one host core: frame ``seed`` of the cfg2 workload through the
-    oracle.  mode 'loop' = the loop-faithful restatement (per-chirp RDS, dechirp.py:196-211; peak dicts,
-    dechirp.py:215-278), then, for peak shard ``shard`` of ``nshard`` (peaks shard::nshard), per-peak eigh MUSIC over
-    the 361-point grid (angle_estimation.py:109-176) and SVD ESPRIT (:178-225); mode 'vector' = the vectorised
-    restatement (fft2, closed-form MUSIC / ESPRIT over all peaks at once).  Returns (azimuths rad, phases, N_p)."""
-    seed, mode, shard, nshard = args
+    """Work item of cpu_baseline's process pool, on one host core: one whole cfg2 frame (seed ``seed``) through the
+    oracle, each stage timed on this core (perf_counter; the frame's synthesis is the input, not timed).
+    mode 'loop' = the loop-faithful restatement: per-chirp RDS (dechirp.py:196-211), peak dicts (dechirp.py:215-278),
+    then per-peak eigh MUSIC over the 361-point grid (angle_estimation.py:109-176) + SVD ESPRIT (:178-225) for the
+    frame's first ``kmax`` peaks (the bounded sample; every peak when kmax <= 0); mode 'vector' = the vectorised
+    restatement (fft2, closed-form MUSIC / ESPRIT over all peaks).  Returns (azimuths rad, phases of the processed
+    peaks, N_p, {stage: seconds}, peaks processed)."""
+    seed, mode, kmax = args
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import radar_oracle as O
     np.random.seed(1000 + seed)
     Tc = 51.2e-6
     frame = O.synthesize_frame(O.TEST_SCENE, chirp_duration=Tc, num_chirps=128, num_antennas=8)
     grid = O.azimuth_grid()
+    t = {}
+    t0 = time.perf_counter()
     if mode == 'loop':
         rds = O.range_doppler_spectrum_loop(frame, chirp_duration=Tc)
+        t1 = time.perf_counter()
         peaks = O.extract_peaks(rds)['peaks']
-        mine = peaks[shard::nshard]
+        t2 = time.perf_counter()
+        mine = peaks if kmax <= 0 else peaks[:kmax]
         az, sig = np.empty(len(mine)), np.empty((len(mine), 8), complex)
         for n, p in enumerate(mine):
             s = O.spatial_signature(rds, p['range_bin'], p['doppler_bin'])
             az[n] = grid[np.argmax(O.music_spectrum_eigh(s, grid))]
             O.esprit_svd(s)
             sig[n] = s
+        t3 = time.perf_counter()
         Np = len(peaks)
     else:
         rds = O.range_doppler_spectrum(frame, chirp_duration=Tc)
+        t1 = time.perf_counter()
         a, i, j, _ = O.peak_arrays(rds)
+        t2 = time.perf_counter()
         sig = rds[:, i, j].T
         sig = sig / np.sqrt(np.sum(np.abs(sig) ** 2, axis=1, keepdims=True))
         steer = O.steering_matrix(grid, 8)
         az = np.concatenate([grid[np.argmax(O.music_spectrum_closed(sig[k:k + 8192], steer), axis=1)]
                              for k in range(0, len(sig), 8192)])
         O.esprit_closed(sig)
+        t3 = time.perf_counter()
         Np = len(a)
-    return np.radians(az), O.observed_phase(sig), Np
+    t.update(rds=t1 - t0, peaks=t2 - t1, doa=t3 - t2)
+    return np.radians(az), O.observed_phase(sig), Np, t, len(sig)
 
 
 def _cpu_model():
@@ -111,50 +125,91 @@ def _cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(procs=16, frames=2, ridge=0.01):
-    """Oracle ('port') chain on whole cfg2 frames, SURVEY §8(d)(ii), on ``procs`` single-threaded worker processes
-    (BLAS threads = 1).  Loop-faithful line: each frame is split into ``procs`` peak shards (work items (frame,
-    shard); every item also runs its frame's RDS + peak extraction, ~1 % of a frame's work, so the line is slightly
-    pessimistic), then the parent solves each frame's LS velocity over all its peaks; value = frames / wall time.
-    Every peak of every frame is processed (no sampling).  A second line times the vectorised restatement, one
-    frame per worker."""
+def host_cores():
+    """(cores this process may use, CPUs in its affinity mask, cgroup CPU quota in cores or None).  A GPU box grants a
+    share of the host (a cgroup cpu.max quota) while the affinity mask and os.cpu_count() show the whole machine."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max', '/sys/fs/cgroup/cpu/cpu.cfs_quota_us'):
+        try:
+            txt = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith('cpu.max') and txt and txt[0] != 'max':
+            quota = int(txt[0]) / int(txt[1])
+        elif path.endswith('quota_us') and txt and int(txt[0]) > 0:
+            quota = int(txt[0]) / int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        break
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, aff, quota
+
+
+def cpu_baseline(procs=0, kmax=3000, vec_frames=2, ridge=0.01):
+    """Oracle ('port') chain on cfg2 frames, SURVEY §8(d)(ii), on all the host cores this process may use (``procs``
+    = 0; host_cores) as single-threaded worker processes (BLAS threads = 1), one whole frame per worker at least.
+
+    Loop-faithful line: P frames, one per worker, each through the per-chirp RDS, the peak dicts and per-peak eigh
+    MUSIC + SVD ESPRIT for its first ``kmax`` peaks (a frame has ~49 k peaks at ~2.6 ms each, 130 core-s: the bounded
+    sample keeps the run near 10 s), then the LS velocity of each frame in the parent.  Every stage is timed on its
+    core while all P workers run together; a frame's seconds = RDS + peaks + (DoA per peak) x N_p + velocity per peak
+    x N_p, and value = P / that (P frames in flight on P cores).  Vectorised line: ``vec_frames`` whole frames per
+    worker, every peak, timed the same way (no extrapolation)."""
     import multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import radar_oracle as O
     for v in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
         os.environ[v] = '1'  # inherited by the spawned workers before they import numpy
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    P = max(1, min(procs, avail))
+    use, aff, quota = host_cores()
+    P = use if procs <= 0 else max(1, min(procs, aff))
     lam = 3e8 / 77e9
     ctx = mp.get_context('spawn')
-    with ctx.Pool(P) as pool:
-        pool.map(_cpu_frame, [(0, 'vector', 0, 1)] * P)  # worker start-up and imports outside the timing
-        t0 = time.perf_counter()
-        res = pool.map(_cpu_frame, [(f, 'loop', k, P) for f in range(frames) for k in range(P)], chunksize=1)
-        nps = []
-        for f in range(frames):
-            part = res[f * P:(f + 1) * P]
-            O.velocity_ls(np.concatenate([r[0] for r in part]), np.concatenate([r[1] for r in part]),
-                          lambda_c=lam, ridge=ridge)
-            nps.append(part[0][2])
-        t_loop = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        vres = pool.map(_cpu_frame, [(f, 'vector', 0, 1) for f in range(P)], chunksize=1)
-        for r in vres:
+
+    def stage_means(res):
+        tv0 = time.perf_counter()
+        for r in res:
             O.velocity_ls(r[0], r[1], lambda_c=lam, ridge=ridge)
-        t_vec = time.perf_counter() - t0
-    return dict(value=frames / t_loop, unit="frames/s", cores=P, kind="port",
-                cpu=_cpu_model(), nproc=os.cpu_count(), cores_available=avail,
-                sample=(f"{frames} whole cfg2 frames (8x128x512; N_p {min(nps)}-{max(nps)}, every peak) on {P} worker "
-                        f"processes x 1 thread: loop-faithful oracle (per-chirp RDS, peak dicts, per-peak eigh MUSIC + "
-                        f"SVD ESPRIT, each frame's peaks sharded over the {P} workers; LS velocity over all peaks); "
-                        f"{t_loop:.1f} s wall, {t_loop * P / frames:.0f} core-s per frame"),
-                vectorised={"value": P / t_vec, "unit": "frames/s", "cores": P,
-                            "sample": f"{P} whole cfg2 frames, one per worker: vectorised oracle (fft2, closed-form "
-                                      f"MUSIC / ESPRIT over all peaks, LS velocity); {t_vec:.1f} s wall"})
+        tvel = (time.perf_counter() - tv0) / max(1, sum(r[4] for r in res))  # LS seconds per processed peak
+        m = {k: float(np.mean([r[3][k] for r in res])) for k in ('rds', 'peaks', 'doa')}
+        m['doa_per_peak'] = float(np.mean([r[3]['doa'] / max(r[4], 1) for r in res]))
+        m['velocity_per_peak'] = tvel
+        m['peaks_per_frame'] = float(np.mean([r[2] for r in res]))
+        return m
+
+    with ctx.Pool(P) as pool:
+        pool.map(_cpu_frame, [(0, 'vector', 0)] * P, chunksize=1)  # worker start-up and imports outside the timing
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_frame, [(f, 'loop', kmax) for f in range(P)], chunksize=1)
+        wall_loop = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        vres = pool.map(_cpu_frame, [(f, 'vector', 0) for f in range(P * vec_frames)], chunksize=1)
+        wall_vec = time.perf_counter() - t0
+    m = stage_means(res)
+    npk = m['peaks_per_frame']
+    frame_s = m['rds'] + m['peaks'] + (m['doa_per_peak'] + m['velocity_per_peak']) * npk
+    mv = stage_means(vres)
+    vframe_s = mv['rds'] + mv['peaks'] + mv['doa'] + mv['velocity_per_peak'] * mv['peaks_per_frame']
+    nproc = [r[4] for r in res]
+    return dict(value=P / frame_s, unit="frames/s", cores=P, kind="port", cpu=_cpu_model(), nproc=os.cpu_count(),
+                cores_available=use, affinity_cpus=aff, cgroup_cpu_quota=quota,
+                seconds_per_frame_per_core={"range_doppler": m['rds'], "peak_extraction": m['peaks'],
+                                            "doa_music_esprit": m['doa_per_peak'] * npk,
+                                            "velocity_ls": m['velocity_per_peak'] * npk, "total": frame_s},
+                sample=(f"{P} whole cfg2 frames (8x128x512), one per worker process x 1 thread, all {P} together "
+                        f"({wall_loop:.1f} s wall): loop-faithful oracle, per-chirp RDS and peak dicts of every "
+                        f"frame timed in full, per-peak eigh MUSIC + SVD ESPRIT and LS velocity timed on the first "
+                        f"{min(nproc)}-{max(nproc)} of the frame's {npk:.0f} peaks and scaled to all of them"),
+                vectorised={"value": P / vframe_s, "unit": "frames/s", "cores": P,
+                            "seconds_per_frame_per_core": {"range_doppler": mv['rds'], "peak_extraction": mv['peaks'],
+                                                           "doa_music_esprit": mv['doa'],
+                                                           "velocity_ls": mv['velocity_per_peak'] * mv['peaks_per_frame'],
+                                                           "total": vframe_s},
+                            "wall_frames_per_s": P * vec_frames / wall_vec,
+                            "sample": f"{P * vec_frames} whole cfg2 frames, {vec_frames} per worker, every peak: "
+                                      f"vectorised oracle (fft2, closed-form MUSIC / ESPRIT, LS velocity); "
+                                      f"{wall_vec:.1f} s wall"})
 
 
 SPEC_PROFILE = os.path.join(ROOT, 'profiles', 'r2b_spectrum_pmc.json')  # tools/profile_spectrum.sh
@@ -170,6 +225,78 @@ def spectrum_traffic(frames):
         if name.startswith('rsl::k_doa_toep') and 'hbm_bytes' in e:
             return e['hbm_bytes'] * frames / prof.get('frames_per_launch', 1000)
     return None
+
+
+def pcie_inclusive(ctx, dev, F=500, steps=8):
+    """The metric's rate when every frame's c64 cube [A, C, S] (4 MiB at cfg2) first crosses PCIe from pinned host
+    memory (SURVEY §8(d) "Timed region": reported beside `value`, never as it).  Host-to-device copies of batch i + 1
+    run on a copy stream while the chain processes batch i; each batch's per-frame velocities come back to pinned host
+    memory.  Also the raw pinned H2D bandwidth and the same loop with the cubes resident."""
+    import torch
+    import rsl
+    A, C, Tc = 8, 128, 51.2e-6
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
+    gen = rsl.SyntheticCubes(ctx, SCENE, chirp_duration=Tc, num_chirps=C, num_antennas=A, noise_power=0.01)
+    host = []
+    for i in range(2):  # two distinct pinned host batches, generated on the device and copied out once
+        d = gen.generate(F, seed=4321, frame0=i * F)
+        torch.cuda.synchronize()
+        h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
+        h.copy_(d)
+        host.append(h)
+        del d
+    dbuf = [torch.empty(host[0].shape, dtype=host[0].dtype, device=dev) for _ in range(2)]
+    vel_d = [torch.empty((F, 8), dtype=torch.float64, device=dev) for _ in range(2)]
+    vel_h = [torch.empty((F, 8), dtype=torch.float64, pin_memory=True) for _ in range(2)]
+    chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel_d[k]) for k in range(2)]
+    nbytes = host[0].numel() * host[0].element_size()
+    cs, ks = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    with torch.cuda.stream(cs):
+        dbuf[0].copy_(host[0], non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(cs):
+        for i in range(4):
+            dbuf[i % 2].copy_(host[i % 2], non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = 4 * nbytes / (time.perf_counter() - t0)
+    ev_copy = [torch.cuda.Event() for _ in range(2)]
+    ev_done = [torch.cuda.Event() for _ in range(2)]
+    used = [False, False]
+
+    def step(i):
+        k = i % 2
+        with torch.cuda.stream(cs):
+            if used[k]:
+                cs.wait_event(ev_done[k])  # batch i - 2 is done with dbuf[k] and vel_d[k]
+                vel_h[k].copy_(vel_d[k], non_blocking=True)
+            dbuf[k].copy_(host[k], non_blocking=True)
+            ev_copy[k].record(cs)
+        with torch.cuda.stream(ks):
+            ks.wait_event(ev_copy[k])
+            chains[k].run(dbuf[k])
+            ev_done[k].record(ks)
+        used[k] = True
+
+    for i in range(2):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    fps = steps * F / (time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(ks):
+        for i in range(steps):
+            chains[i % 2].run(dbuf[i % 2])
+    torch.cuda.synchronize()
+    fps_res = steps * F / (time.perf_counter() - t0)
+    return {"value": fps, "unit": "frames/s", "frames_per_batch": F, "steps": steps,
+            "bytes_per_frame": nbytes // F, "h2d_pinned_GBps": h2d / 1e9,
+            "pcie_bound_frames_per_s": h2d / (nbytes / F), "device_resident_same_loop_frames_per_s": fps_res,
+            "what": "cfg2 chain, c64 cubes copied host -> device per batch (pinned memory, copy stream overlapped "
+                    "with the previous batch's chain), velocities copied back; one compute stream"}
 
 
 def cu_masked_stream(dev, ncu, side, total=256):
@@ -277,9 +404,11 @@ def main():
                          'the full MUSIC spectrum of every cell, f32 [G, cells]); the last two are second '
                          'measurements, not the metric line')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-frames', type=int, default=2, help='whole frames of the loop-faithful CPU baseline')
-    ap.add_argument('--cpu-procs', type=int, default=16,
-                    help='worker processes of the CPU baseline (the GPU box grants 16 host cores per GPU)')
+    ap.add_argument('--no-pcie', action='store_true', help='skip the PCIe-inclusive side measurement')
+    ap.add_argument('--cpu-peaks', type=int, default=3000,
+                    help='peaks per frame through the loop-faithful CPU DoA (the bounded sample; <= 0: every peak)')
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='worker processes of the CPU baseline (0: every host core this process may use)')
     ap.add_argument('--ridge', type=float, default=0.01,
                     help='ridge on (v_x, v_y) of the LS velocity solve (configs[2]: "regularised LS"; the 0.01 of '
                          'velocity_solver_improved.py:261); 0 = the plain VelocitySolver LS')
@@ -461,29 +590,38 @@ def main():
         Fl = F // NS
         ncl = nc / NS                                          # unique cells per launch
         # Roofline entries of the three big kernels.  Algorithmic work per launch (per kernel):
-        #  K1 k_range_fft_p: read the c64 cube + write the c64 range spectra  = 2 A C S 8 bytes per frame
-        #  K2 k_doppler_detect: read the range spectra + write the c64 RDS    = 2 A C S 8 bytes per frame
-        #     (masks / peak powers, ~1 %, not counted)
+        #  K1 (k_range_fft_r512 at cfg2): read the c64 cube (8 B per value) + write the packed range spectra (6 B
+        #     per value + one exponent byte per 8 values)                                 = A C S 14.125 bytes per frame
+        #  K2 (k_doppler_detect_r128): read the packed spectra of 16 + 2 halo range bins per 16-bin tile + write the
+        #     c64 RDS (masks / peak powers, ~1 %, not counted)                 = A C S (6.125 x 18 / 16 + 8) per frame
+        #  (c64 `work` at other shapes: k_range_fft_p / k_doppler_detect, 2 A C S 8 bytes per frame each)
         #  K5 k_doa_toep: one real dot product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2),
         #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
         src_std = ks if ks else kt
+        packed = (C, S) == (128, 512)
+        # the kernels implementing K1 / K2 for this shape: packed `work` at cfg2 (rsl_fft.hip work_packed_supported)
+        fft_names = ({'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'} if packed
+                     else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
         per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
         flops = 3 * 2 * (2 * A - 1) * ncl * G
-        kbytes = 2 * A * C * S * 8 * Fl
+        kbytes = ({'range_fft': A * C * S * 14.125 * Fl, 'doppler_fft': A * C * S * (6.125 * 18 / 16 + 8) * Fl}
+                  if packed else {'range_fft': 2 * A * C * S * 8 * Fl, 'doppler_fft': 2 * A * C * S * 8 * Fl})
 
         def entry(name, ms):
             if name == 'doa_scan':
                 ach = flops / (ms * 1e-3) / 1e12
                 return {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                        "traffic": pmc_traffic('k_doa_toep', Fl, args.config), "avg_launch_ms": ms,
+                        "traffic": pmc_traffic('k_doa_toep', Fl, args.config), "traffic_source": TRAFFIC_SOURCE,
+                        "avg_launch_ms": ms,
                         "algorithmic_flops_per_launch": flops,
                         "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
-            kern = {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'}[name]
-            ach = kbytes / (ms * 1e-3) / 1e9
+                kern = fft_names[name]
+            ach = kbytes[name] / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, args.config), "avg_launch_ms": ms,
-                    "design_bytes_per_launch": kbytes,
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, args.config),
+                    "traffic_source": TRAFFIC_SOURCE, "avg_launch_ms": ms,
+                    "design_bytes_per_launch": kbytes[name],
                     "note": "per-kernel design bytes (cube or work in, work or RDS out): the work round trip counts "
                             "here, so these fractions are kernel efficiencies, not the stage's algorithmic roofline"}
 
@@ -494,7 +632,6 @@ def main():
         # intermediate between K1 and K2 is NOT algorithmic: it shows up as traffic above the algorithmic bytes.
         big = ('range_fft', 'doppler_fft', 'doa_scan')
         fft_k = [k for k in ('range_fft', 'doppler_fft') if k in kt and kt[k][1]]
-        fft_names = {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'}
         fft_bytes = 2 * A * C * S * 8 * Fl
 
         def stage(src, timed):
@@ -503,7 +640,7 @@ def main():
             return {"bound": "hbm", "kernels": [fft_names[k] for k in fft_k],
                     "achieved": fft_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": fft_bytes / t / 1e9 / HBM_PEAK_GBS,
-                    "traffic": None if any(x is None for x in tr) else sum(tr),
+                    "traffic": None if any(x is None for x in tr) else sum(tr), "traffic_source": TRAFFIC_SOURCE,
                     "avg_launch_ms": t * 1e3, "algorithmic_bytes_per_launch": fft_bytes, "timed": timed}
 
         line["roofline"] = stage(kt, "hipEvents over the timed region (pipelined: the stage co-runs with the "
@@ -515,9 +652,11 @@ def main():
         line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
         if ks:
             line["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
+    if not args.no_pcie and world == 1 and args.config == 'cfg2':
+        line["pcie_inclusive"] = pcie_inclusive(ctx, dev)
     if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed on rank 0 at N = 1 only
         try:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_procs, args.cpu_frames, ridge=args.ridge)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_procs, args.cpu_peaks, ridge=args.ridge)
         except Exception as e:  # the baseline is reported, never the target
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

@@ -334,8 +334,9 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
 // Stockham passes through LDS.  The LDS FFT was LDS-bound (SQ_LDS_IDX_ACTIVE ~70 % of the kernel's cycles, 21 % of wave
 // time waiting on LDS issue, 42 % extra bank-conflict cycles): staging + 3 stage writes + 3 stage reads + the output
 // read.  Here a tile (8 chirp rows of one (frame, antenna)) takes two LDS exchanges, both conflict-free:
-//   a tile is chirp class c of one (frame, antenna): the 8 chirps c + 16 q (q < 8; C = 128, c < 16), so that K2's
-//   Doppler transform can start with a radix-8 step in registers (k_doppler_detect_r128);
+//   a tile is chirp class c of one (frame, antenna): the 8 chirps c + 16 q (q < 8; C = 128, c < 16), so that the
+//   Doppler transform's radix-8 step over q (and its W128^(c k1) twiddle) runs here, in registers, at the packed
+//   store; K2 (k_doppler_detect_r128) does the 16-point step over the classes;
 //   x[n], n = j + 32 m (j < 32, m < 16), thread t = (row q = t / 32, j = t % 32) loads x[j + 32 m] of chirp c + 16 q
 //   (8-B loads, two 256-B runs per wave instruction) and multiplies by conj(ref) w;
 //   stage 1: V[j][k1] = DFT16_m x[j + 32 m]  (registers), times W512^(j k1) (LDS table, 17-float2 pitch per j);
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
 //   stage 2: thread t = (row, k1 = (t / 2) % 16, h = t % 2) takes j = 2 i + h: E or O = DFT16_i (registers); lane
 //   pairs swap halves by DPP and form X[k1 + 16 k2] = E + W32^k2 O, X[k1 + 16 (k2 + 16)] = E - W32^k2 O;
 //   output: X -> obuf[row][b + 8 (b / 256)] (the b >= 256 half shifted by 8: conflict-free writes), then thread p
-//   reads bins 2p, 2p + 1 of the 8 rows (16-B reads) and stores them packed (pk_pack16).
+//   reads bins 2p, 2p + 1 of the 8 rows (16-B reads), takes W128^(c k1) DFT8_q of each and stores them packed.
 // X[k1 + 16 k2'] = sum_j W512^(j k1) W32^(j k2') sum_m x[j + 32 m] W16^(m k1): the 512-point DFT exactly.
 // DBG (development builds only; wrong results): 2 no cube loads, 3 loads only.
 constexpr int kR512Pitch = 34;             // xbuf pitch per (row, k1): 32 j + 2 pad
@@ -442,19 +443,35 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
 #pragma unroll
     for (int k = 0; k < 16; ++k) ow[16 * k] = xo[k];
     __syncthreads();
-    // packed store: thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows
-    float f0[16], f1[16];
-    unsigned m0 = 0u, m1 = 0u;
+    // thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows (chirps cb + 16 q): the Doppler transform's first step,
+    // Y[k1] = W128^(cb k1) DFT8_q, here in registers (K2 starts from the 16-point step)
+    float2 y0[8], y1[8];
     const int pos = 2 * tid + (tid >= 128 ? 8 : 0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float4 ab = *reinterpret_cast<const float4*>(obuf + q * kR512Obuf + pos);
-      f0[2 * q] = ab.x;
-      f0[2 * q + 1] = ab.y;
-      f1[2 * q] = ab.z;
-      f1[2 * q + 1] = ab.w;
-      m0 = max(m0, max(__float_as_uint(ab.x) & 0x7FFFFFFFu, __float_as_uint(ab.y) & 0x7FFFFFFFu));
-      m1 = max(m1, max(__float_as_uint(ab.z) & 0x7FFFFFFFu, __float_as_uint(ab.w) & 0x7FFFFFFFu));
+      y0[q] = make_float2(ab.x, ab.y);
+      y1[q] = make_float2(ab.z, ab.w);
+    }
+    Dft<8>::run(y0);
+    Dft<8>::run(y1);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float2 wk = tw[4 * cb * k];  // W128^(cb k) = W512^(4 cb k), 4 cb k <= 420 (workgroup-uniform)
+      y0[k] = cmul(y0[k], wk);
+      y1[k] = cmul(y1[k], wk);
+    }
+    // packed store
+    float f0[16], f1[16];
+    unsigned m0 = 0u, m1 = 0u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      f0[2 * q] = y0[q].x;
+      f0[2 * q + 1] = y0[q].y;
+      f1[2 * q] = y1[q].x;
+      f1[2 * q + 1] = y1[q].y;
+      m0 = max(m0, max(__float_as_uint(y0[q].x) & 0x7FFFFFFFu, __float_as_uint(y0[q].y) & 0x7FFFFFFFu));
+      m1 = max(m1, max(__float_as_uint(y1[q].x) & 0x7FFFFFFFu, __float_as_uint(y1[q].y) & 0x7FFFFFFFu));
     }
     const int e0 = pk_exp(m0), e1 = pk_exp(m1);
     uint4 w0[3], w1[3];
@@ -623,12 +640,13 @@ constexpr bool dd_reg_ok() {
 // the tile's compacted peak powers are staged in the dead LDS tile and stored block-wide (tools/pkb.sh).
 // DBG (development builds only, ablations with wrong results): 4 no peak-power stores, 5 no mask / count stores,
 // 8 no RDS stores, 9 RDS stores only (no detection).
-template <int C, int KB, int NT, int DBG = 0>
+// LD / PADC: the tile's row pitch and whether columns sit at padded positions lp(d) (the LDS Stockham FFT's layout) or
+// at d (k_doppler_detect_r128).
+template <int C, int KB, int NT, int DBG = 0, int LD = lp_row(C) | 1, bool PADC = true>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
                                  int* __restrict__ row_count, float* __restrict__ dbmap,
                                  float* __restrict__ pk_pow, int tid_in = -1) {
-  constexpr int LD = lp_row(C) | 1;
   constexpr int NCH = C / 64;
   // tid_in: a laundered thread index from a persistent caller (keeps per-thread addresses out of its tile loop)
   const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -640,7 +658,7 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   if (i0 >= S) i0 -= S;
   const int rb = rh * 8;  // LDS rows rb .. rb + 9; interior rows rb + 1 .. rb + 8
   float p[10];
-  const float2* col = buf + lp(d);
+  const float2* col = buf + (PADC ? lp(d) : d);
   float2* dst = rds + ((size_t)fa * S + i0 + rb) * C + j;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -840,30 +858,34 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 }
 
 // K2 + K3 for C = 128 with packed `work` (the cfg2 shape): the Doppler FFT as 8 x 16 in registers.  K1 stores chirp
-// class c (chirps c + 16 r, r < 8) as one packed tile, so thread (bin b, class c) = (tid % 16, tid / 16) loads the 8
-// chirps x[c + 16 r] of its bin (3 x 16 B) and
-//   stage 1: Y_c[k1] = DFT8_r x[c + 16 r] (registers), times W128^(c k1) (the twiddle table in LDS, broadcast reads);
+// class c (chirps c + 16 r, r < 8) as one packed tile after the first radix-8 step, Y'_c[k1] = W128^(c k1) DFT8_r
+// x[c + 16 r] (k_range_fft_r512), so thread (bin b, class c) = (tid % 16, tid / 16) loads the 8 values of its bin
+// (3 x 16 B) and
 //   exchange: Y' -> xb[c][k1][b2] (b2 = LDS row: b + 1, halo rows 0 and 17 from threads 0-31), 144 float2 per class;
 //   stage 2: thread t < 144 = (k1 = t / 18, b2 = t % 18) reads xb[c][t] for c < 16 (consecutive per instruction),
 //   X[k1 + 8 k2] = DFT16_c (registers), written to the tile row b2 at the unshifted Doppler position;
 // then the register-form detection (dd_tile_compute_reg) as in k_doppler_detect.  X[k1 + 8 k2] = sum_c W128^(c k1)
 // W16^(c k2) sum_r x[c + 16 r] W8^(r k1): the 128-point DFT exactly.  Against the LDS Stockham form (staging + two
 // stage passes) a third less LDS traffic.  DBG (development builds only): 6 no work loads, 7 loads only.
-template <int DBG = 0>
-__global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __restrict__ work, int S,
+template <int KB, int DBG = 0>
+__global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* __restrict__ work, int S,
                                                             const float2* __restrict__ tw, float2* __restrict__ rds,
                                                             float thr_f, int i_lo, int i_hi,
                                                             unsigned long long* __restrict__ mask,
                                                             int* __restrict__ row_count, float* __restrict__ dbmap,
                                                             float* __restrict__ pk_pow,
                                                             const unsigned char* __restrict__ wexp) {
-  constexpr int C = 128, KB = 16, NT = 256, NR = KB + 2, NCB = 16;
-  constexpr int LD = lp_row(C) | 1;
-  constexpr int XP = 8 * NR;  // xb floats2 per class
+  constexpr int C = 128, NT = 16 * KB, NR = KB + 2, NCB = 16;
+  static_assert(KB == 16 || KB == 32, "one unit (bin, class) per thread; the halo from threads 0-31");
+  // rows of C + 1 float2, columns unpadded (the stage-2 row writes of 16-lane groups hit 16 distinct banks); the
+  // per-class exchange pitch 8 NR + 1 (the halo threads' writes, one class per lane, hit distinct banks).  19 KB of
+  // LDS: 8 workgroups per CU
+  constexpr int LD = C + 1;
+  constexpr int NP = 8 * NR;  // (k1, b2) pairs per class
+  constexpr int XP = NP + 1;  // xb float2 per class
   static_assert(NCB * XP <= NR * LD, "exchange buffer must fit in the tile buffer");
   extern __shared__ float2 sm[];
-  float2* tws = sm;
-  float2* buf = sm + C;
+  float2* buf = sm;
   float2* xb = buf;  // exchange, then the tile rows (aliased: a barrier separates the last read from the first write)
   const int tid = threadIdx.x;
   const unsigned nkb = (unsigned)(S / KB);
@@ -885,8 +907,7 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
     }
     e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cls) * (size_t)S + k];
   };
-  const float2 twv = tw[tid & (C - 1)];
-  const int b = tid & 15, cls = tid >> 4;
+  const int b = tid % KB, cls = tid / KB;
   uint4 wi[3], wh[3];
   int ei, eh = 0;
   unit(k0 + b, cls, wi, ei);
@@ -897,32 +918,24 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
     kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
     unit(kk, hcls, wh, eh);
   }
-  if (tid < C) tws[tid] = twv;
-  __syncthreads();  // twiddles
   if constexpr (DBG == 7) {
     if (__uint_as_float(wi[0].x ^ wh[1].y) == 1.2345e30f) rds[tid] = make_float2((float)ei, (float)eh);
     return;
   }
-  // stage 1 for one unit: decode, DFT8 over r, twiddle W128^(c k1), write xb[c][k1][b2]
+  // one unit (K1 stored Y'_c[k1] = W128^(c k1) DFT8_r already): decode, write xb[c][k1][b2]
   auto stage1 = [&](const uint4(&w)[3], int e, int c, int b2) {
     float f[16];
     pk_unpack16(w, pk_pow2(e - 22), f);
-    float2 y[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) y[r] = make_float2(f[2 * r], f[2 * r + 1]);
-    Dft<8>::run(y);
-#pragma unroll
-    for (int k = 1; k < 8; ++k) y[k] = cmul(y[k], tws[c * k]);
     float2* dst = xb + c * XP + b2;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dst[k * NR] = y[k];
+    for (int k = 0; k < 8; ++k) dst[k * NR] = make_float2(f[2 * k], f[2 * k + 1]);
   };
   stage1(wi, ei, cls, b + 1);
   if (halo) stage1(wh, eh, hcls, hside ? NR - 1 : 0);
   __syncthreads();
   // stage 2: DFT16 over the classes
   float2 x[16];
-  const bool s2 = tid < XP;
+  const bool s2 = tid < NP;
   const int k1 = tid / NR, b2 = tid - (tid / NR) * NR;
   if (s2) {
 #pragma unroll
@@ -933,10 +946,10 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
   if (s2) {
     float2* row = buf + b2 * LD;
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) row[lp(k1 + 8 * k2)] = x[k2];
+    for (int k2 = 0; k2 < 16; ++k2) row[k1 + 8 * k2] = x[k2];
   }
   __syncthreads();
-  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0>(
+  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false>(
       buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
 }
 
@@ -954,9 +967,6 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
   // One tile per workgroup, 256 threads.  Measured and not kept: a persistent variant with a register prefetch of the
   // next tile (5.0-5.25 vs 3.85 ms per 2000 cfg2 frames), a 320-thread block (2.72 vs 2.48 ms per 1000 frames).
   auto kern = k_doppler_detect<C, KB, NT, true>;
-  if constexpr (C == 128 && KB == 16) {
-    if (wexp) kern = k_doppler_detect_r128<>;  // packed work (work_packed_supported): register-form transform
-  }
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
     const int v = atoi(e);
@@ -967,14 +977,6 @@ static hipError_t launch_k2d_kb(hipStream_t st, const float2* work, int F, int A
     if (v == 5) kern = k_doppler_detect<C, KB, NT, true, 5>;
     if (v == 6) kern = k_doppler_detect<C, KB, NT, true, 6>;
     if (v == 7) kern = k_doppler_detect<C, KB, NT, true, 7>;
-    if constexpr (C == 128 && KB == 16) {
-      if (wexp && v == 4) kern = k_doppler_detect_r128<4>;
-      if (wexp && v == 5) kern = k_doppler_detect_r128<5>;
-      if (wexp && v == 6) kern = k_doppler_detect_r128<6>;
-      if (wexp && v == 7) kern = k_doppler_detect_r128<7>;
-      if (wexp && v == 8) kern = k_doppler_detect_r128<8>;
-      if (wexp && v == 9) kern = k_doppler_detect_r128<9>;
-    }
   }
 #endif
   // tile-compact peak powers from the register tile body (KB rows per group), row-compact from the general body
@@ -993,10 +995,52 @@ static int dd_kb(int C, int S) {
   return kb;
 }
 
+// K2 + K3 on packed work (work_packed_supported: C = 128, S = 512), k_doppler_detect_r128 with KR range bins per tile.
+template <int KR>
+static hipError_t launch_k2d_r128(hipStream_t st, const float2* work, int F, int A, int S, float2* rds, double thr_p,
+                                  int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
+                                  float* pk_pow, int* pk_group, const unsigned char* wexp) {
+  constexpr int C = 128, NT = 16 * KR;
+  static_assert(dd_reg_ok<C, KR, NT>(), "register tile body shape");
+  const long ntile = (long)F * A * (S / KR);
+  // unpadded C + 1 rows + the register body's exchange area (edge columns and ballots: 16 B per row per 64 columns)
+  const size_t lds = sizeof(float2) * (size_t)(KR + 2) * (C + 1) + (size_t)KR * (C / 64) * 16;
+  const float thr_f = threshold_as_float(thr_p);
+  auto kern = k_doppler_detect_r128<KR>;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
+    const int v = atoi(e);
+    if (v == 4) kern = k_doppler_detect_r128<KR, 4>;
+    if (v == 5) kern = k_doppler_detect_r128<KR, 5>;
+    if (v == 6) kern = k_doppler_detect_r128<KR, 6>;
+    if (v == 7) kern = k_doppler_detect_r128<KR, 7>;
+    if (v == 8) kern = k_doppler_detect_r128<KR, 8>;
+    if (v == 9) kern = k_doppler_detect_r128<KR, 9>;
+  }
+#endif
+  *pk_group = KR;  // tile-compact peak powers (dd_tile_compute_reg)
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, nullptr, rds, thr_f, i_lo, i_hi, mask,
+                     row_count, dbmap, pk_pow, wexp);
+  return hipGetLastError();
+}
+
 template <int C>
 static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
                              double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
                              float* pk_pow, int* pk_group, const unsigned char* wexp) {
+  if constexpr (C == 128) {
+    if (wexp) {
+      // 16 range bins per tile: 2.59 ms per 2000 cfg2 frames against 2.67 for 32 (512 threads, half the halo reads)
+#ifdef RSL_DEV_KNOBS
+      if (const char* e = getenv("RSL_R128_KB"))
+        if (atoi(e) == 32)
+          return launch_k2d_r128<32>(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow,
+                                     pk_group, wexp);
+#endif
+      return launch_k2d_r128<16>(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group,
+                                 wexp);
+    }
+  }
   constexpr int K0 = rows_for(C);
   constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
   if (dd_kb(C, S) == K1)

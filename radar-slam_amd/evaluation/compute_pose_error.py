@@ -17,6 +17,7 @@ on the host, as plain numpy on a handful of numbers.
 from __future__ import annotations
 
 import logging
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -192,16 +193,15 @@ class PoseErrorEvaluator:
 
 def evaluate_pose_errors(estimated_path: str, ground_truth_path: str, output_path: str,
                          timestamps_path: Optional[str] = None) -> Dict:
-    """File wrapper (:520-588).  As in the reference, ``os`` is only imported under ``__main__`` (:594), so a
-    truthy ``timestamps_path`` raises NameError when this module is imported; and the PoseIntegrator's Euler
-    'orientations' [N, 3] give [N, 6] poses, whose quaternion columns raise ValueError."""
+    """File wrapper (:520-588).  The reference imports ``os`` only under ``__main__`` (:594), so an imported module
+    raises NameError on a truthy ``timestamps_path``; here (as in compute_velocity_error.py) ``os`` is imported at
+    module level and the timestamps load works on both routes.  The PoseIntegrator's Euler 'orientations' [N, 3]
+    give [N, 6] poses, whose quaternion columns raise ValueError, as in the reference."""
     est_d = np.load(estimated_path, allow_pickle=True)
     gt_d = np.load(ground_truth_path, allow_pickle=True)
     est = np.column_stack([est_d['positions'], est_d['orientations']])
     gt = np.column_stack([gt_d['positions'], gt_d['orientations']])
-    timestamps = None
-    if timestamps_path:
-        raise NameError("name 'os' is not defined")
+    timestamps = np.load(timestamps_path) if timestamps_path and os.path.exists(timestamps_path) else None
     ev = PoseErrorEvaluator()
     ape = ev.compute_ape(est, gt)
     rte = ev.compute_rte(est, gt, timestamps)
@@ -210,3 +210,16 @@ def evaluate_pose_errors(estimated_path: str, ground_truth_path: str, output_pat
     np.savez(output_path, ape_metrics=ape, rte_metrics=rte, report=report)
     logger.info(f"Pose error evaluation complete: {output_path}")
     return {'ape_metrics': ape, 'rte_metrics': rte}
+
+
+if __name__ == "__main__":
+    import argparse
+
+    p = argparse.ArgumentParser(description='Evaluate pose errors')
+    p.add_argument('--est', required=True, help='Path to estimated poses')
+    p.add_argument('--gt', required=True, help='Path to ground truth poses')
+    p.add_argument('--out', required=True, help='Output path for evaluation')
+    p.add_argument('--timestamps', help='Path to timestamps file')
+    a = p.parse_args()
+    res = evaluate_pose_errors(a.est, a.gt, a.out, a.timestamps)
+    print(f"Pose error evaluation complete: {res['ape_metrics']['pose_rmse']:.6f}")

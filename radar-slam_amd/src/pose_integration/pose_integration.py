@@ -62,8 +62,15 @@ class PoseIntegrator:
         N = len(v)
         if N == 0:
             np.zeros((0, 3))[0] = self.initial_position  # the reference's positions[0] = ... on an empty array
-        ctx, pos, _ = _scan(v.reshape(N, -1)[:, :3], min(3, v.reshape(N, -1).shape[1]), None, timestamps,
-                            _METHODS[self.integration_method])
+        # the reference adds velocities[i] (shape [k], or a scalar for 1-D input) to a 3-vector (:88, :97): a scalar or
+        # k = 1 broadcasts to x, y, z; any other k != 3 raises numpy's broadcast error once the loop runs (N >= 2)
+        v = v.reshape(N, -1) if v.ndim != 1 else v[:, None]
+        k = v.shape[1]
+        if k != 3:
+            if k != 1 and N >= 2:
+                raise ValueError(f'operands could not be broadcast together with shapes (3,) ({k},) ')
+            v = np.repeat(v, 3, axis=1) if k == 1 else np.zeros((N, 3))
+        ctx, pos, _ = _scan(v, 3, None, timestamps, _METHODS[self.integration_method])
         pos += ctx.torch.as_tensor(self.initial_position, dtype=ctx.torch.float64, device=pos.device)
         if self.smoothing and N > self.smoothing_window:
             from rsl.traj import smooth

@@ -185,6 +185,10 @@ def test_pose_integration_dropin_needs_device(golden):
         PoseIntegrator().integrate_translational_velocity(z['vel'], z['ts'])
     with pytest.raises(ValueError, match='Unknown integration method'):
         PoseIntegrator(integration_method='rk4').integrate_translational_velocity(z['vel'], z['ts'])
+    # [N, 2] velocities: the reference's 3-vector + 2-vector broadcast error (pose_integration.py:88), before any
+    # device work
+    with pytest.raises(ValueError, match='broadcast'):
+        PoseIntegrator().integrate_translational_velocity(z['vel'][:, :2], z['ts'])
 
 
 def test_product_path_has_no_oracle_import():
