@@ -616,7 +616,7 @@ def main():
                         "avg_launch_ms": ms,
                         "algorithmic_flops_per_launch": flops,
                         "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
-                kern = fft_names[name]
+            kern = fft_names[name]
             ach = kbytes[name] / (ms * 1e-3) / 1e9
             return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, args.config),
