@@ -150,6 +150,30 @@ RSL_DEV void toep_split(const float (&ar)[MA], const float (&ai)[MA], float inv,
   }
 }
 
+// atan2 for the fused extras: |t| = min / max reduced to [0, 1], atan(t) = t + t z P(z) (z = t^2, P of degree 7,
+// least-squares fit, max error 9e-8 rad in fp32 evaluation) and the octant / quadrant fixes.  About half the VALU of
+// the library atan2f (no frexp-scaled division, no inf / nan cases: the inputs are finite); within 1e-7 rad of it,
+// four orders below the 1e-3 rad DoA tolerance.  atan2(+-0, x < 0) = +-pi, atan2(y, +-0) as atan2f except y = x = 0
+// (0 here).
+RSL_DEV float atan2_fast(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float t = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+  const float z = t * t;
+  float p = 0.00262275873683393f;
+  p = fmaf(p, z, -0.015134590677917004f);
+  p = fmaf(p, z, 0.041125182062387466f);
+  p = fmaf(p, z, -0.07366984337568283f);
+  p = fmaf(p, z, 0.10574059933423996f);
+  p = fmaf(p, z, -0.14186006784439087f);
+  p = fmaf(p, z, 0.19990399479866028f);
+  p = fmaf(p, z, -0.3333298861980438f);
+  float a = fmaf(t * z, p, t);
+  a = ay > ax ? 1.57079632679489662f - a : a;
+  a = x < 0.f ? 3.14159265358979324f - a : a;
+  return copysignf(a, y);
+}
+
 // v_permlane32_swap on each dword: the upper 32 lanes of a are exchanged with the lower 32 lanes of b.
 RSL_DEV void swap32_u4(uint4& a, uint4& b) {
   unsigned av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
@@ -260,7 +284,7 @@ RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __res
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false,
           bool SPEC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : (SPEC ? 1 : 3)))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (DBG == 11 ? 3 : 4) : (SPEC ? 1 : 3)))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
@@ -288,7 +312,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
   // Two-level prefetch: the signature of the next pass is loaded during this pass from cell indices that were loaded
   // one pass earlier (index loads followed at once by the dependent signature loads stalled every pass for a full
   // memory round trip).
-  float2 ns[MA];
+  constexpr bool PD2 = DBG == 11;  // ablation: signatures prefetched two passes ahead
+  float2 ns[MA], ns2[PD2 ? MA : 1];
   int2 nidx = make_int2(0, 0);
   if (ch < nch) {
     const long long c = ch * 64 + lane;
@@ -298,7 +323,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     } else {
       load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
       const long long c2 = (ch + stride) * 64 + lane;
-      if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
+      if constexpr (PD2) {
+        if (ch + stride < nch) load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns2);
+        const long long c4 = (ch + 2 * stride) * 64 + lane;
+        if (ch + 2 * stride < nch) nidx = load_cell(cfr, crc, c4, c4 < ncell);
+      } else {
+        if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
+      }
     }
   }
   // The argmax (and gmax) of a pass is stored at the start of the NEXT pass, after the wait for that pass's prefetched
@@ -317,7 +348,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
     }
     const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
-    if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
+    if constexpr (PD2) {
+#pragma unroll
+      for (int m = 0; m < MA; ++m) ns[m] = ns2[m];
+      if (nx + stride < nch) {
+        load_sig_at<MA>(rds, nidx, A, plane, fstride, ns2);
+        const long long c5 = (nx + 2 * stride) * 64 + lane;
+        if (nx + 2 * stride < nch) nidx = load_cell(cfr, crc, c5, c5 < ncell);
+      }
+    } else if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
+      if constexpr (DBG == 10) nidx = make_int2(0, nidx.y & 2047);  // ablation: L2-resident signatures
       load_sig_at<MA>(rds, nidx, A, plane, fstride, ns);
       const long long c3 = (nx + stride) * 64 + lane;
       if (nx + stride < nch) nidx = load_cell(cfr, crc, c3, c3 < ncell);
@@ -344,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
             }
             esprit_phi<MA>(sr, si, A, nr, ni, dd);
           }
-          const float ang = dd > 0.f ? atan2f(ni, nr) : 0.f;
+          const float ang = dd > 0.f ? atan2_fast(ni, nr) : 0.f;
           // fp32 asin (the input angle is fp32 already; tolerance 1e-3 rad).  For d >= lambda/2 the reference's
           // argument never exceeds 1 (|angle| <= pi): clamp the fp32 rounding of pi * scale there; for d < lambda/2
           // |x| > 1 gives NaN as in the reference.
@@ -353,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
           out_esprit[c] = (double)(asinf(x) * 57.2957795130823208768f);
         }
         if (out_phase)
-          out_phase[c] = (double)atan2f(s[1].y * s[0].x - s[1].x * s[0].y, s[1].x * s[0].x + s[1].y * s[0].y);
+          out_phase[c] = (double)atan2_fast(s[1].y * s[0].x - s[1].x * s[0].y, s[1].x * s[0].x + s[1].y * s[0].y);
       }
     }
     // B operands of the two column tiles: own K half from the own cell, the other half from lane ^ 32
@@ -492,7 +532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         }
       }
     };
-    if constexpr (SKEW && NTC > 0 && KB == 1 && DBG == 0) {
+      if constexpr (SKEW && NTC > 0 && KB == 1 && (DBG == 0 || DBG == 1 || DBG == 3 || DBG >= 8)) {
       // Skewed schedule: the two column tiles' MFMA chains run half a tile apart, so each chain's epilogue (tile max,
       // record test, record copy) issues while the other chain's MFMAs execute instead of waiting for them; the A
       // operands of tile t + 1 are read from LDS during tile t's first epilogue.  Same products and record order.
@@ -511,7 +551,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc, 0, 0, 0);
       };
       auto rec = [&](int t, const floatx16& acc, float& best, int& bt, double (&sv)[8]) {
+        if constexpr (DBG == 8) {  // no epilogue: one max per tile keeps the accumulator live
+          best = fmaxf(best, acc[t & 15]);
+          return;
+        }
         const float m = tile_max(acc);
+        if (t == 0) {
+          typedef double doublex8 __attribute__((ext_vector_type(8)));
+          const doublex8 d = __builtin_bit_cast(doublex8, acc);
+          best = m;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sv[k] = d[k];
+          return;
+        }
+        if (m > best) {
+          best = m;
+          bt = t;
+          if constexpr (DBG != 1) copy_tile(sv, acc);
+        }
+      };
+      // record commit after the tile max m of a column tile's accumulator (first tile: unconditional)
+      auto commit = [&](int t, float m, const floatx16& acc, float& best, int& bt, double (&sv)[8]) {
         if (t == 0) {
           typedef double doublex8 __attribute__((ext_vector_type(8)));
           const doublex8 d = __builtin_bit_cast(doublex8, acc);
@@ -526,6 +586,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
           copy_tile(sv, acc);
         }
       };
+      if constexpr (DBG == 9) {  // no tile loop (prologue, loads and the index resolution only)
+        best0 = __builtin_bit_cast(float, b0h[0].x ^ b1l[0].y);
+        best1 = __builtin_bit_cast(float, b1h[0].z ^ b0l[0].w);
+      } else if constexpr (DBG == 12) {
+        // Interleaved skew: each column tile's tile-max VALU is issued BETWEEN the other column tile's three MFMAs
+        // (one MFMA, three VALU, ...) instead of as a block after them, so that the matrix pipe keeps running while
+        // the wave does its epilogue; the record copies (a branch) follow each group.  Pipeline per tile t:
+        //   [chain1(t) | max(acc0(t))] -> copy0(t) -> [max(acc1(t)) | chain0(t + 1)] -> copy1(t)
+        // Same products, same record order as the block schedule.
+        lda(0);
+        chain(acc0, x0h, x0l);
+#pragma unroll
+        for (int t = 0; t < NTC; ++t) {
+          __builtin_amdgcn_sched_barrier(0);
+          chain(acc1, x1h, x1l);
+          const float m0 = tile_max(acc0);
+          const bool r0 = t == 0 || m0 > best0;
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < NTC) lda(t + 1);
+          if (r0) commit(t, m0, acc0, best0, bt0, sv0);
+          __builtin_amdgcn_sched_barrier(0);
+          const float m1 = tile_max(acc1);
+          const bool r1 = t == 0 || m1 > best1;
+          if (t + 1 < NTC) {
+            chain(acc0, x0h, x0l);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (r1) commit(t, m1, acc1, best1, bt1, sv1);
+        }
+      } else {
       lda(0);
       chain(acc0, x0h, x0l);
       chain(acc1, x1h, x1l);
@@ -542,6 +644,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
         spec_tile(t, acc1, 1);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NTC) chain(acc1, x1h, x1l);
+      }
       }
     } else {
       const int ntl = NTC ? NTC : ntiles;  // NTC: compile-time tile count (fully unrolled loop)
@@ -610,15 +713,17 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
     if (ntiles == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true>;
   }
 #ifdef RSL_DEV_KNOBS
-  if constexpr (MUSIC && !GMAX && !EXTRAS && !SPEC && MA == 8) {  // RSL_DOA_DBG: ablation variants (timing only)
+  if constexpr (MUSIC && !GMAX && !SPEC && MA == 8) {  // RSL_DOA_DBG: ablation variants of the skewed kernel (timing)
     if (const char* e = getenv("RSL_DOA_DBG")) {
       const int v = atoi(e);
-      if (ntiles == 12) {  // the unrolled form the bench runs
-        if (v == 1) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 1, 12>;
-        if (v == 2) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 2, 12>;
-        if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3, 12>;
-        if (v == 4) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 4, 12>;
-        if (v == 7) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 7, 12>;
+      if (ntiles == 12) {
+        if (v == 1) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 1, 12, true>;  // no record-tile copies
+        if (v == 3) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 3, 12, true>;  // no signature loads
+        if (v == 8) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 8, 12, true>;  // no argmax epilogue
+        if (v == 9) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 9, 12, true>;  // no tile loop
+        if (v == 10) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 10, 12, true>;  // L2-resident signatures
+        if (v == 11) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 11, 12, true>;  // prefetch 2 passes ahead
+        if (v == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 12, 12, true>;  // interleaved skew
       }
     }
   }
