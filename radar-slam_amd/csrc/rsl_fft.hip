@@ -867,15 +867,18 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 // then the register-form detection (dd_tile_compute_reg) as in k_doppler_detect.  X[k1 + 8 k2] = sum_c W128^(c k1)
 // W16^(c k2) sum_r x[c + 16 r] W8^(r k1): the 128-point DFT exactly.  Against the LDS Stockham form (staging + two
 // stage passes) a third less LDS traffic.  DBG (development builds only): 6 no work loads, 7 loads only.
-template <int KB, int DBG = 0>
-__global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* __restrict__ work, int S,
+template <int KB, int DBG = 0, int TPW = 1>
+__global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* __restrict__ work, int S_arg,
                                                             const float2* __restrict__ tw, float2* __restrict__ rds,
                                                             float thr_f, int i_lo, int i_hi,
                                                             unsigned long long* __restrict__ mask,
                                                             int* __restrict__ row_count, float* __restrict__ dbmap,
                                                             float* __restrict__ pk_pow,
                                                             const unsigned char* __restrict__ wexp) {
-  constexpr int C = 128, NT = 16 * KB, NR = KB + 2, NCB = 16;
+  // S = 512 wherever this kernel runs (work_packed_supported): the tile index math folds to shifts and masks instead of
+  // a runtime 32-bit division (≈ 200 SALU per wave before)
+  constexpr int C = 128, S = 512, NT = 16 * KB, NR = KB + 2, NCB = 16;
+  (void)S_arg;
   static_assert(KB == 16 || KB == 32, "one unit (bin, class) per thread; the halo from threads 0-31");
   // rows of C + 1 float2, columns unpadded (the stage-2 row writes of 16-lane groups hit 16 distinct banks); the
   // per-class exchange pitch 8 NR + 1 (the halo threads' writes, one class per lane, hit distinct banks).  19 KB of
@@ -888,14 +891,10 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
   float2* buf = sm;
   float2* xb = buf;  // exchange, then the tile rows (aliased: a barrier separates the last read from the first write)
   const int tid = threadIdx.x;
-  const unsigned nkb = (unsigned)(S / KB);
-  const unsigned tile = (unsigned)xcd_tile(blockIdx.x, gridDim.x);
-  const int kb = (int)(tile % nkb);
-  const unsigned fa = tile / nkb;
-  const int k0 = kb * KB;
+  constexpr unsigned nkb = (unsigned)(S / KB);
+  const unsigned g = (unsigned)xcd_tile(blockIdx.x, gridDim.x);  // TPW consecutive tiles g TPW + i per workgroup
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
-  const size_t tile0 = (size_t)fa * NCB;
-  auto unit = [&](int k, int cls, uint4(&w)[3], int& e) {
+  auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3], int& e) {
     const uint4* src =
         reinterpret_cast<const uint4*>(wb + (tile0 + cls) * kPkTile + (size_t)(3 * (k & 1)) * kPkPlane) + (k >> 1);
 #pragma unroll
@@ -908,18 +907,27 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
     e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cls) * (size_t)S + k];
   };
   const int b = tid % KB, cls = tid / KB;
-  uint4 wi[3], wh[3];
-  int ei, eh = 0;
-  unit(k0 + b, cls, wi, ei);
   const bool halo = tid < 2 * NCB;  // threads 0-31: (side, class) = (tid / 16, tid % 16)
   const int hside = tid >> 4, hcls = tid & 15;
-  if (halo) {
-    int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
-    kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
-    unit(kk, hcls, wh, eh);
+  // every tile's loads issued before the first tile's transform (TPW > 1: the later tiles' loads are in flight
+  // during the earlier tiles' transforms and stores)
+  uint4 wi[TPW][3], wh[TPW][3];
+  int ei[TPW], eh[TPW];
+#pragma unroll
+  for (int q = 0; q < TPW; ++q) {
+    const unsigned tile = g * TPW + q;
+    const int k0 = (int)(tile % nkb) * KB;
+    const size_t tile0 = (size_t)(tile / nkb) * NCB;
+    unit(tile0, k0 + b, cls, wi[q], ei[q]);
+    eh[q] = 0;
+    if (halo) {
+      int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
+      kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+      unit(tile0, kk, hcls, wh[q], eh[q]);
+    }
   }
   if constexpr (DBG == 7) {
-    if (__uint_as_float(wi[0].x ^ wh[1].y) == 1.2345e30f) rds[tid] = make_float2((float)ei, (float)eh);
+    if (__uint_as_float(wi[0][0].x ^ wh[0][1].y) == 1.2345e30f) rds[tid] = make_float2((float)ei[0], (float)eh[0]);
     return;
   }
   // one unit (K1 stored Y'_c[k1] = W128^(c k1) DFT8_r already): decode, write xb[c][k1][b2]
@@ -930,27 +938,35 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
 #pragma unroll
     for (int k = 0; k < 8; ++k) dst[k * NR] = make_float2(f[2 * k], f[2 * k + 1]);
   };
-  stage1(wi, ei, cls, b + 1);
-  if (halo) stage1(wh, eh, hcls, hside ? NR - 1 : 0);
-  __syncthreads();
-  // stage 2: DFT16 over the classes
-  float2 x[16];
   const bool s2 = tid < NP;
   const int k1 = tid / NR, b2 = tid - (tid / NR) * NR;
-  if (s2) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) x[c] = xb[c * XP + tid];
-    Dft<16>::run(x);
-  }
-  __syncthreads();  // xb reads done: the tile rows alias it
-  if (s2) {
-    float2* row = buf + b2 * LD;
+  for (int q = 0; q < TPW; ++q) {
+    const unsigned tile = g * TPW + q;
+    const int k0 = (int)(tile % nkb) * KB;
+    const unsigned fa = tile / nkb;
+    if (q > 0) __syncthreads();  // the previous tile's body is done with the LDS tile
+    stage1(wi[q], ei[q], cls, b + 1);
+    if (halo) stage1(wh[q], eh[q], hcls, hside ? NR - 1 : 0);
+    __syncthreads();
+    // stage 2: DFT16 over the classes
+    float2 x[16];
+    if (s2) {
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) row[k1 + 8 * k2] = x[k2];
+      for (int c = 0; c < 16; ++c) x[c] = xb[c * XP + tid];
+      Dft<16>::run(x);
+    }
+    __syncthreads();  // xb reads done: the tile rows alias it
+    if (s2) {
+      float2* row = buf + b2 * LD;
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) row[k1 + 8 * k2] = x[k2];
+    }
+    __syncthreads();
+    dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false>(
+        buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap,
+        pk_pow);
   }
-  __syncthreads();
-  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false>(
-      buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
 }
 
 template <int C, int KB>
@@ -1002,7 +1018,9 @@ static hipError_t launch_k2d_r128(hipStream_t st, const float2* work, int F, int
                                   float* pk_pow, int* pk_group, const unsigned char* wexp) {
   constexpr int C = 128, NT = 16 * KR;
   static_assert(dd_reg_ok<C, KR, NT>(), "register tile body shape");
+  if (S != 512) return hipErrorInvalidValue;  // the kernel's tile math is compiled for S = 512 (work_packed_supported)
   const long ntile = (long)F * A * (S / KR);
+  int tpw = 1;  // tiles per workgroup (development builds: RSL_R128_TPW=2)
   // unpadded C + 1 rows + the register body's exchange area (edge columns and ballots: 16 B per row per 64 columns)
   const size_t lds = sizeof(float2) * (size_t)(KR + 2) * (C + 1) + (size_t)KR * (C / 64) * 16;
   const float thr_f = threshold_as_float(thr_p);
@@ -1017,10 +1035,15 @@ static hipError_t launch_k2d_r128(hipStream_t st, const float2* work, int F, int
     if (v == 8) kern = k_doppler_detect_r128<KR, 8>;
     if (v == 9) kern = k_doppler_detect_r128<KR, 9>;
   }
+  if (const char* e = getenv("RSL_R128_TPW"))
+    if (atoi(e) == 2) {
+      kern = k_doppler_detect_r128<KR, 0, 2>;
+      tpw = 2;
+    }
 #endif
   *pk_group = KR;  // tile-compact peak powers (dd_tile_compute_reg)
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, nullptr, rds, thr_f, i_lo, i_hi, mask,
-                     row_count, dbmap, pk_pow, wexp);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(ntile / tpw)), dim3(NT), lds, st, work, S, nullptr, rds, thr_f, i_lo, i_hi,
+                     mask, row_count, dbmap, pk_pow, wexp);
   return hipGetLastError();
 }
 

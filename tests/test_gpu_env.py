@@ -18,7 +18,7 @@ OLD_SWITCHES = {
     'RSL_DD_CP': '0', 'RSL_DD_KB': '32', 'RSL_DD_XCD': '0', 'RSL_DD_LDS': '65536', 'RSL_DD_PAD': '0',
     'RSL_DD_PERSIST': '1', 'RSL_DD_DBG': '2', 'RSL_DOA_SKEW': '0', 'RSL_DOA_PPW': '0', 'RSL_DOA_FULL': '1',
     'RSL_DOA_BPC': '1', 'RSL_DOA_UNROLL': '0', 'RSL_DOA_DBG': '1', 'RSL_EMIT_CELLS': '0', 'RSL_EMIT_WPE': '0',
-    'RSL_OFF_NT': '1024',
+    'RSL_OFF_NT': '1024', 'RSL_WORK_C64': '1', 'RSL_R128_KB': '32', 'RSL_R128_TPW': '2',
 }
 
 
