@@ -1,0 +1,45 @@
+"""bench.py's host-side measurement pieces on CPU (no device): the CPU baseline's structure and arithmetic on a tiny
+sample, the host-core detection, and the PMC traffic lookup (named kernels only, stale profiles give None)."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_host_cores_reports_quota_or_affinity():
+    import bench
+    use, aff, quota = bench.host_cores()
+    assert 1 <= use <= aff
+    assert quota is None or use == max(1, min(aff, int(quota)))
+
+
+def test_cpu_baseline_structure_small():
+    import bench
+    r = bench.cpu_baseline(procs=2, kmax=8, vec_frames=1, ridge=0.01)
+    assert r['kind'] == 'port' and r['cores'] == 2 and r['unit'] == 'frames/s'
+    st = r['seconds_per_frame_per_core']
+    assert set(st) == {'range_doppler', 'peak_extraction', 'doa_music_esprit', 'velocity_ls', 'total'}
+    assert abs(st['total'] - (st['range_doppler'] + st['peak_extraction'] + st['doa_music_esprit'] + st['velocity_ls'])) \
+        < 1e-9 * st['total']
+    assert r['value'] == pytest.approx(2 / st['total'])
+    v = r['vectorised']
+    assert v['cores'] == 2 and v['value'] == pytest.approx(2 / v['seconds_per_frame_per_core']['total'])
+    assert 'first 8-8 of the frame' in r['sample']
+
+
+def test_pmc_traffic_named_kernels(tmp_path, monkeypatch):
+    import bench
+    prof = {'frames_per_launch': 2000, 'kernels': {
+        'rsl::k_range_fft_r512<true, 0>': {'hbm_bytes': 14.8e9},
+        'rsl::k_doppler_detect_r128<16, 0>': {'hbm_bytes': 15.4e9}}}
+    p = tmp_path / 'p.json'
+    p.write_text(json.dumps(prof))
+    monkeypatch.setattr(bench, 'PROFILE', str(p))
+    assert bench.pmc_traffic('k_range_fft_r512', 1000) == pytest.approx(7.4e9)
+    assert bench.pmc_traffic('k_doppler_detect_r128', 2000) == pytest.approx(15.4e9)
+    assert bench.pmc_traffic('k_range_fft_p', 2000) is None  # a kernel the profile does not name: no bytes
+    assert bench.pmc_traffic('k_range_fft_r512', 2000, config='cfg5') is None
