@@ -373,7 +373,8 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
   const int tid = threadIdx.x;
   const int row = tid >> 5, j = tid & 31;
   const int k1b = (tid >> 1) & 15, h = tid & 1;
-  const int ncb = C / CB;
+  constexpr int ncb = 128 / CB;  // C = 128 wherever this kernel runs (work_packed_supported): tile index math by shifts
+  (void)C;
   const long G = gridDim.x;
   for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
   for (int k = tid; k < 32 * 16; k += kThreads) {
@@ -1086,6 +1087,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     size_t lds_k = lds;
     if constexpr (S == 512 && CB == 8) {
       if (wexp) {  // packed work (work_packed_supported): the register-form 16 x 32 transform
+        if (C != 128) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 128
         kern = k_range_fft_r512<true>;
         lds_k = 0;  // static LDS only
       }

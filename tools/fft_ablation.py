@@ -45,9 +45,11 @@ def timed(env):
 variants = []
 for c64 in (os.environ.get('C64', '1,0')).split(','):
     only0 = os.environ.get('ONLY0') == '1'  # the full kernels only (A/B of two libraries)
-    for rf in ('0',) if only0 else ('0', '1', '2', '3'):
+    rfl = os.environ.get('RF_LIST')  # explicit variant lists, e.g. RF_LIST=0,5
+    ddl = os.environ.get('DD_LIST')
+    for rf in rfl.split(',') if rfl else ('0',) if only0 else ('0', '1', '2', '3'):
         variants.append(('K1', {'RSL_WORK_C64': c64, 'RSL_RF_DBG': rf}))
-    for dd in ('0',) if only0 else ('0', '1', '4', '5', '6', '7') + (('8', '9') if c64 == '0' else ()):
+    for dd in ddl.split(',') if ddl else ('0',) if only0 else ('0', '1', '4', '5', '6', '7') + (('8', '9') if c64 == '0' else ()):
         variants.append(('K2', {'RSL_WORK_C64': c64, 'RSL_DD_DBG': dd}))
 best = {}
 for rep in range(3):
