@@ -34,6 +34,7 @@ PROFILE = os.path.join(ROOT, 'profiles', 'r3c_pmc.json')  # rocprofv3 FETCH_SIZE
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
+STANDALONE_RUNS = 6  # unpipelined chain runs after the timed region (kernel_ms_standalone, fft_stage_standalone)
 TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
                   ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')
 
@@ -552,7 +553,7 @@ def main():
     ks = {}  # standalone kernel times: the pipelined timed region overlaps the two halves of consecutive batches
     if kt and args.pipeline:
         ctx.timing_reset()
-        for i in range(2):
+        for i in range(STANDALONE_RUNS):  # one chain at a time on one stream; per-kernel means over these runs
             chains[0].run(cubes[i % nb])
         torch.cuda.synchronize()
         ks = ctx.timing_read()
@@ -646,7 +647,7 @@ def main():
         line["roofline"] = stage(kt, "hipEvents over the timed region (pipelined: the stage co-runs with the "
                                      "previous batch's DoA scan)" if args.pipeline else "hipEvents over the timed region")
         if ks:
-            line["fft_stage_standalone"] = stage(ks, "standalone launches after the timed region")
+            line["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
         line["roofline_doa"] = entry('doa_scan', per('doa_scan'))
         line["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big}
         line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
