@@ -68,6 +68,23 @@ RSL_DEV void vel_load(long long i0, long long e, const int* __restrict__ gidx, c
   }
 }
 
+// Order-preserving key of a finite or infinite double (NaN never enters): min / max of keys = min / max of values.
+RSL_DEV unsigned long long okey(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+RSL_DEV double unkey(unsigned long long k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// One workgroup per frame.  gidx path (the chain): one pass over the cells.  Besides the 7 moments it keeps, per grid
+// index g, the smallest and largest phase of the cells with weight > 0 (LDS min / max on order-preserving keys:
+// exact and order-independent).  All cells of index g share the prediction p_g = k (vx c_g + vy s_g), so the
+// residual y - p_g of largest magnitude is that of the group's smallest or largest y: max |residual| comes from 2G
+// values instead of a second pass over the cells (bit-identical: same p_g, same subtraction).  The residual sum
+// of squares is the quadratic form of the moments; it is used when its terms do not cancel (R2 >= 1e-6 of their
+// magnitude sum, i.e. < 1e-9 relative rounding), else (a near-perfect fit) R2 is summed per cell in a second pass,
+// as it is for the az path and whenever per-cell residuals / predictions are requested.
 __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az, const int* __restrict__ gidx,
                                                   const double* __restrict__ az_table, int G,
                                                   const double* __restrict__ y, const unsigned* __restrict__ amask,
@@ -77,11 +94,20 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
                                                   double* __restrict__ pred) {
   __shared__ double sh[8];
   __shared__ double mom[7];
-  __shared__ double sol[2];
-  extern __shared__ double cs_tab[];  // [2G] cos, sin of the grid azimuths (gidx path)
+  __shared__ double sol[3];
+  extern __shared__ double cs_tab[];  // [2G] cos, sin of the grid azimuths, then [2G] min / max phase keys (gidx path)
   const bool tab = gidx != nullptr;
+  const bool grp = tab;  // per-group extremes: 32 G B of LDS (rsl_velocity admits G <= 2048)
+  unsigned long long* ymn = reinterpret_cast<unsigned long long*>(cs_tab + 2 * G);
+  unsigned long long* ymx = ymn + G;
   if (tab) {
-    for (int g = threadIdx.x; g < G; g += blockDim.x) sincos(az_table[g], &cs_tab[G + g], &cs_tab[g]);
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+      sincos(az_table[g], &cs_tab[G + g], &cs_tab[g]);
+      if (grp) {
+        ymn[g] = ~0ull;
+        ymx[g] = 0ull;  // no key is 0 (that would be a NaN's bits): 0 marks an empty group
+      }
+    }
     __syncthreads();
   }
   const long f = blockIdx.x;
@@ -106,7 +132,14 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
       unsigned mv[kVelU];
       vel_load(i0, e, gidx, y, amask, gv, yv, mv);
 #pragma unroll
-      for (int u = 0; u < kVelU; ++u) acc1((double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+      for (int u = 0; u < kVelU; ++u) {
+        acc1((double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+        if (grp && mv[u] != 0u && yv[u] == yv[u]) {  // weight > 0, not NaN (fmax ignores a NaN residual)
+          const unsigned long long kk = okey(yv[u]);
+          atomicMin(&ymn[gv[u]], kk);
+          atomicMax(&ymx[gv[u]], kk);
+        }
+      }
     }
   } else {
     for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
@@ -159,9 +192,15 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
     }
     sol[0] = bx;
     sol[1] = by;
+    // residual sum of squares from the moments, kept when its terms do not cancel (gidx path only)
+    const double kx = k * bx, ky = k * by;
+    const double q = m[6] - 2.0 * (kx * m[4] + ky * m[5]) + kx * kx * m[1] + 2.0 * kx * ky * m[2] + ky * ky * m[3];
+    const double mag = m[6] + 2.0 * (fabs(kx * m[4]) + fabs(ky * m[5])) + kx * kx * m[1] + 2.0 * fabs(kx * ky * m[2]) +
+                       ky * ky * m[3];
+    sol[2] = (grp && q >= 1e-6 * mag) ? q : -1.0;
   }
   __syncthreads();
-  const double vx = sol[0], vy = sol[1];
+  const double vx = sol[0], vy = sol[1], r2m = sol[2];
   double r2 = 0.0, rmax = 0.0;
   auto acc2 = [&](long long i, double w, double c, double s, double yi) {
     const double pr = k * (vx * c + vy * s);
@@ -172,15 +211,24 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
     if (pred) pred[i] = pr;
   };
   if (tab) {
-    for (long long i0 = b + threadIdx.x; i0 < e; i0 += step) {
-      int gv[kVelU];
-      double yv[kVelU];
-      unsigned mv[kVelU];
-      vel_load(i0, e, gidx, y, amask, gv, yv, mv);
+    if (!grp || r2m < 0.0 || resid || pred) {
+      for (long long i0 = b + threadIdx.x; i0 < e; i0 += step) {
+        int gv[kVelU];
+        double yv[kVelU];
+        unsigned mv[kVelU];
+        vel_load(i0, e, gidx, y, amask, gv, yv, mv);
 #pragma unroll
-      for (int u = 0; u < kVelU; ++u)
-        if (i0 + (long long)u * blockDim.x < e)
-          acc2(i0 + (long long)u * blockDim.x, (double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+        for (int u = 0; u < kVelU; ++u)
+          if (i0 + (long long)u * blockDim.x < e)
+            acc2(i0 + (long long)u * blockDim.x, (double)__popc(mv[u]), cs_tab[gv[u]], cs_tab[G + gv[u]], yv[u]);
+      }
+    }
+    if (grp) rmax = 0.0;  // from the per-group extremes (same values as the per-cell maximum)
+    for (int g = threadIdx.x; grp && g < G; g += blockDim.x) {
+      const unsigned long long hi = ymx[g];
+      if (hi == 0ull) continue;
+      const double pr = k * (vx * cs_tab[g] + vy * cs_tab[G + g]);
+      rmax = fmax(rmax, fmax(fabs(unkey(ymn[g]) - pr), fabs(unkey(hi) - pr)));
     }
   } else {
     for (long long i = b + threadIdx.x; i < e; i += blockDim.x) {
@@ -189,7 +237,8 @@ __global__ __launch_bounds__(512) void k_velocity(const double* __restrict__ az,
       acc2(i, amask ? (double)__popc(amask[i]) : 1.0, c, s, y[i]);
     }
   }
-  const double R2 = block_sum(r2, sh);
+  const double R2s = block_sum(r2, sh);
+  const double R2 = r2m >= 0.0 ? r2m : R2s;
   const double RM = block_max(rmax, sh);
   if (threadIdx.x == 0) {
     double* o = out + f * 8;
@@ -208,7 +257,7 @@ hipError_t launch_velocity(hipStream_t st, const double* az, const int* gidx, co
                            const double* y, const unsigned* amask, const long long* seg, long long n, int F, double k, double ridge,
                            const double* bounds4, double* out, double* resid, double* pred) {
   if (F <= 0) return hipSuccess;
-  const size_t lds = gidx ? sizeof(double) * 2 * (size_t)G : 0;
+  const size_t lds = gidx ? sizeof(double) * 4 * (size_t)G : 0;
   hipLaunchKernelGGL(k_velocity, dim3(F), dim3(512), lds, st, az, gidx, az_table, G, y, amask, seg, n, k, ridge,
                      bounds4[0], bounds4[1], bounds4[2], bounds4[3], out, resid, pred);
   return hipGetLastError();

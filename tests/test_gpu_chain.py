@@ -148,6 +148,12 @@ def test_velocity_parity(runs, name):
         assert abs(v[2] - cost) <= P.VEL_COST_RTOL * cost
         assert abs(v[0] - vx) < P.VEL_ATOL and abs(v[1] - vy) < P.VEL_ATOL
         assert int(v[5]) == len(y)
+        # rmse and max |residual| (velocity_solver.py:283-284) at the GPU's own solution: the kernel takes max |r| from
+        # per-grid-index phase extremes and the residual sum of squares from its moments
+        k = 4 * np.pi * 0.1 / (3e8 / cfg.fc)
+        res = y - k * (v[0] * np.cos(az) + v[1] * np.sin(az))
+        assert abs(v[3] - np.sqrt(res @ res / len(y))) <= 1e-9 * max(1.0, v[3])
+        assert abs(v[4] - np.abs(res).max()) <= 1e-12 * max(1.0, v[4])
 
 
 def _oracle_argmax(sigs, steer, chunk=20000):
