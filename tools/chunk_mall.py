@@ -1,0 +1,82 @@
+"""FFT stage (K1 + K2) over one 2000-frame cfg2 batch: one launch pair vs chunks of N frames on two alternating
+streams, each stream with its own librsl handle (own K1 dequeue counters) and a chunk-sized `work` buffer.  With
+small chunks the `work` a chunk's K1 writes is read back by its K2 while fewer than ~256 MiB of other bytes have
+passed through the Infinity Cache, so the round trip could be served on-die.  Outputs (RDS, masks, row counts,
+peak powers) must be bit-identical to the one-launch run.  GPU box:  python tools/chunk_mall.py  (CHUNKS=4,8,16)"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'radar-slam_amd'), ROOT]
+import torch  # noqa: E402
+
+import rsl  # noqa: E402
+from rsl.runtime import Context  # noqa: E402
+from bench import make_cubes  # noqa: E402
+
+F = int(os.environ.get('F', '2000'))
+A, C, S = 8, 128, 512
+ctx = rsl.get_context(0)
+ctx2 = Context(0)
+cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=51.2e-6)
+ch = rsl.RadarChain(cfg, F, ctx)
+cube = make_cubes(ctx, 1, F, A, C, 51.2e-6, 0)[0]
+e = ctx.empty
+outs = [dict(rds=e((F, A, S, C), torch.complex64), mask=e((F, A, S, 2), torch.int64),
+             row_count=e((F, A, S), torch.int32), peak_pow=e((F, A, S, C), torch.float32)) for _ in range(2)]
+for o in outs:
+    o['peak_pow'].zero_()  # row-compact: only each row's first row_count values are written
+s_main = torch.cuda.current_stream()
+streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+
+def one(o):
+    ctx.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=o['rds'], work=ch.work, mask=o['mask'],
+                   row_count=o['row_count'], peak_pow=o['peak_pow'], dc_removal=True)
+
+
+def chunked(o, n, works):
+    ev = torch.cuda.Event()
+    ev.record(s_main)
+    for s in streams:
+        s.wait_event(ev)
+    for c, c0 in enumerate(range(0, F, n)):
+        c1 = min(F, c0 + n)
+        k = c & 1
+        with torch.cuda.stream(streams[k]):
+            (ctx, ctx2)[k].rds_detect(cube[c0:c1], ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=o['rds'][c0:c1],
+                                      work=works[k], mask=o['mask'][c0:c1], row_count=o['row_count'][c0:c1],
+                                      peak_pow=o['peak_pow'][c0:c1], dc_removal=True)
+    for s in streams:
+        ev2 = torch.cuda.Event()
+        ev2.record(s)
+        s_main.wait_event(ev2)
+
+
+def timed(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        fn()
+    t1.record()
+    torch.cuda.synchronize()
+    return t0.elapsed_time(t1) / reps
+
+
+res = {}
+for rnd in range(3):
+    res.setdefault('one', []).append(timed(lambda: one(outs[0])))
+    for n in [int(x) for x in os.environ.get('CHUNKS', '4,8,16,32').split(',')]:
+        works = [e((n, A, C, S), torch.complex64) for _ in range(2)]
+        res.setdefault(n, []).append(timed(lambda: chunked(outs[1], n, works)))
+        torch.cuda.synchronize()
+        same = all(torch.equal(outs[0][key].view(torch.int32) if outs[0][key].is_complex() else outs[0][key],
+                               outs[1][key].view(torch.int32) if outs[1][key].is_complex() else outs[1][key])
+                   for key in ('mask', 'row_count'))
+        same = same and torch.equal(torch.view_as_real(outs[0]['rds']), torch.view_as_real(outs[1]['rds']))
+        same = same and torch.equal(outs[0]['peak_pow'], outs[1]['peak_pow'])
+        res.setdefault(f'same{n}', []).append(bool(same))
+    print(rnd, {k: (round(v[-1], 3) if not isinstance(v[-1], bool) else v[-1]) for k, v in res.items()}, flush=True)
+print('min over rounds (ms per 2000 frames):', {k: round(min(v), 3) for k, v in res.items() if not str(k).startswith('same')})
