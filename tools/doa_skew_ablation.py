@@ -1,7 +1,8 @@
 """K5 (k_doa_toep, the skewed 12-tile kernel the chain runs) ablations on one cfg2 batch, development library
 (RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so): RSL_DOA_DBG 1 = no record-tile copies, 3 = no signature loads,
 8 = no argmax epilogue (one max per tile), 9 = no tile loop; each with the fused extras (ESPRIT + phase, as the chain
-runs it) and without ('noext').  Results of 1-9 are wrong by construction; only the times matter."""
+runs it) and without ('noext').  Results of 1-9 are wrong by construction; only the times matter (EXACT=0,... lists the variants whose grid indices
+are compared with the chain's)."""
 import json
 import os
 import sys
@@ -45,7 +46,7 @@ for rnd in range(3):
             torch.cuda.synchronize()
             key = f"dbg{v}{'' if ext else '_noext'}"
             res.setdefault(key, []).append(e0.elapsed_time(e1) / 5)
-            if v == '0' and rnd == 0:
+            if v in os.environ.get('EXACT', '0').split(',') and rnd == 0:
                 nc = int(ch.totals()[1])
                 res[key + '_idx_equal'] = bool(torch.equal(idx[:nc], ref_idx[:nc]))
 os.environ.pop('RSL_DOA_DBG')
