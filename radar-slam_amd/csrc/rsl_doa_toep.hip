@@ -92,7 +92,8 @@ RSL_DEV void esprit_acf(const float2 (&s)[MA], const float (&ar)[MA], const floa
   const float hr = (s0.x * s1.x + s0.y * s1.y) * sc, hi = (s0.x * s1.y - s0.y * s1.x) * sc;
   const float a = r0 - el, cc = r0 - e0, br = r1r, bi = r1i;
   const float hd = 0.5f * (a - cc);
-  const float l1 = 0.5f * (a + cc) + sqrtf(hd * hd + br * br + bi * bi);
+  // v_sqrt_f32 directly (1 ulp; the ESPRIT tolerance is 1e-3 rad): the IEEE sqrtf expansion is ~15 VALU per cell
+  const float l1 = 0.5f * (a + cc) + __builtin_amdgcn_sqrtf(hd * hd + br * br + bi * bi);
   float v0r, v0i, v1r, v1i;
   if (a >= cc) {  // v = [l1 - c, conj(b)]
     v0r = l1 - cc; v0i = 0.f; v1r = br; v1i = -bi;
@@ -219,14 +220,14 @@ RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ 
 // order-preserving for non-negative floats, and a tile max is one of its inputs exactly.  P = |a^H s|^2 >= 0; a
 // rounding-negative value can only lose to a positive one, and a tile whose values are all <= 0 never holds the
 // spectrum maximum of a non-zero signature.  (fmaxf on MFMA outputs costs NaN-canonicalising v_max_f32 ops.)
-RSL_DEV float tile_max(const floatx16& a) {
+RSL_DEV float tile_max(const floatx16& a, float lo = __int_as_float(INT_MIN)) {
   int v[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = __float_as_int(a[i]);
   auto mx3 = [](int x, int y, int z) { return max(max(x, y), z); };
   const int m0 = mx3(v[0], v[1], v[2]), m1 = mx3(v[3], v[4], v[5]), m2 = mx3(v[6], v[7], v[8]);
   const int m3 = mx3(v[9], v[10], v[11]), m4 = mx3(v[12], v[13], v[14]);
-  return __int_as_float(mx3(mx3(m0, m1, m2), mx3(m3, m4, v[15]), INT_MIN));
+  return __int_as_float(mx3(mx3(m0, m1, m2), mx3(m3, m4, v[15]), __float_as_int(lo)));
 }
 
 // Record-tile copy for the lanes that set a new record: 8 v_pk_mov_b32 (64-bit pairs) under the branch's exec mask
@@ -555,17 +556,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
           best = fmaxf(best, acc[t & 15]);
           return;
         }
-        const float m = tile_max(acc);
         if (t == 0) {
           typedef double doublex8 __attribute__((ext_vector_type(8)));
           const doublex8 d = __builtin_bit_cast(doublex8, acc);
-          best = m;
+          best = tile_max(acc);
 #pragma unroll
           for (int k = 0; k < 8; ++k) sv[k] = d[k];
           return;
         }
-        if (m > best) {
-          best = m;
+        // the running best joins the max tree (same 8 v_max3): mb = max(best, tile) updates best without a move in
+        // the record branch; mb > best <=> the tile max > best (the tile max as ints is mb whenever it wins)
+        const float mb = tile_max(acc, best);
+        const bool r = mb > best;
+        best = mb;
+        if (r) {
           bt = t;
           if constexpr (DBG != 1) copy_tile(sv, acc);
         }
