@@ -407,7 +407,9 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     float2 v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 32 * m]);
-    if (tn < hi) load(nx, tn);  // in flight during this tile's transforms and stores
+    // in flight during this tile's transforms and stores; unconditional (past the range: this tile again, an L2 hit
+    // once per workgroup), which spares a copy of the 32 loaded registers per tile
+    load(nx, tn < hi ? tn : t);
     if constexpr (DBG == 3) {
       if (v[0].x == 1.2345e30f) work[tid] = v[1];
       if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
