@@ -96,9 +96,42 @@ __device__ long long block_scan_global(const int* in, int* out, int n, long long
   const int t = threadIdx.x;
   const int per = (n + NT - 1) / NT;
   const int b = t * per, e = min(n, b + per);
+  long long total;
+  if (per % 4 == 0 && n % per == 0 && ((reinterpret_cast<size_t>(in) | reinterpret_cast<size_t>(out)) & 15) == 0) {
+    // whole 16-B runs per thread (e.g. the A * S = 4096 row counts of a cfg2 frame: 4 int4 per thread, each thread's
+    // 64-B segment read and written by 16-B accesses instead of 16 lane-strided 4-B ones)
+    const int4* in4 = reinterpret_cast<const int4*>(in);
+    int4* out4 = reinterpret_cast<int4*>(out);
+    const int q0 = b >> 2, nq = (e - b) >> 2;
+    int4 v[8];
+    long long s = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nq) {
+        v[q] = in4[q0 + q];
+        s += (long long)v[q].x + v[q].y + v[q].z + v[q].w;
+      }
+    for (int q = 8; q < nq; ++q) {  // long runs (per > 32): a second pass over the rest
+      const int4 x = in4[q0 + q];
+      s += (long long)x.x + x.y + x.z + x.w;
+    }
+    long long run = block_exscan<NT>(s, lds, &total);
+    auto put = [&](int q, const int4& x) {
+      int4 o;
+      o.x = (int)run; run += x.x;
+      o.y = (int)run; run += x.y;
+      o.z = (int)run; run += x.z;
+      o.w = (int)run; run += x.w;
+      out4[q0 + q] = o;
+    };
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nq) put(q, v[q]);
+    for (int q = 8; q < nq; ++q) put(q, in4[q0 + q]);
+    return total;
+  }
   long long s = 0;
   for (int k = b; k < e; ++k) s += in[k];
-  long long total;
   long long run = block_exscan<NT>(s, lds, &total);
   for (int k = b; k < e; ++k) {
     const int v = in[k];
@@ -121,6 +154,21 @@ __global__ __launch_bounds__(NT) void k_offsets(const unsigned long long* __rest
   const long f = blockIdx.x;
   const long long te = block_scan_global<NT>(row_count + f * A * S, entry_row_off + f * A * S, A * S, lds);
   const unsigned long long* mf = mask + (size_t)f * A * S * W;
+  if (W == 2) {  // C = 65..128 (cfg2): a row's two words as one 16-B load / store
+    const ulonglong2* mf2 = reinterpret_cast<const ulonglong2*>(mf);
+    ulonglong2* um2 = umask ? reinterpret_cast<ulonglong2*>(umask + (size_t)f * S * 2) : nullptr;
+    for (int i = threadIdx.x; i < S; i += NT) {
+      ulonglong2 u = make_ulonglong2(0ull, 0ull);
+#pragma unroll 8
+      for (int a = 0; a < A; ++a) {
+        const ulonglong2 x = mf2[(size_t)a * S + i];
+        u.x |= x.x;
+        u.y |= x.y;
+      }
+      if (um2) um2[i] = u;
+      cell_row_cnt[f * S + i] = __popcll(u.x) + __popcll(u.y);
+    }
+  } else
   for (int i = threadIdx.x; i < S; i += NT) {
     int c = 0;
     for (int w = 0; w < W; ++w) {
@@ -437,6 +485,9 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
   for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
   if (t == 0) s_first = cell_base[f] + cell_row_off[row];
   const unsigned sm16 = (unsigned)(m >> (16 * sl)) & 0xffffu;
+  unsigned sa[MAXA];  // this thread's 16-bit slice of every antenna's word: 32-bit bit extracts per cell below
+#pragma unroll
+  for (int aa = 0; aa < MAXA; ++aa) sa[aa] = (unsigned)(ma[aa] >> (16 * sl)) & 0xffffu;
   int total;
   const int loc = block_exclusive_scan(__popc(sm16), wsum, total);
   {
@@ -445,10 +496,9 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
     while (mm) {
       const int b = __ffs(mm) - 1;
       mm &= mm - 1;
-      const int bit = 16 * sl + b;
       unsigned am = 0;
 #pragma unroll
-      for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> bit) & 1ull) << aa;
+      for (int aa = 0; aa < MAXA; ++aa) am |= ((sa[aa] >> b) & 1u) << aa;
       if constexpr (PACK) {
         pk[o] = ((unsigned)t << 4) | (unsigned)b | (am << 12);
       } else {
