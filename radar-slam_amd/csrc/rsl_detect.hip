@@ -518,9 +518,10 @@ __global__ __launch_bounds__(256) void k_emit_cells(const unsigned long long* __
       const long long g2 = gw0 + (tt >> 2);
       const long long rw = g2 / W;
       const int ww = (int)(g2 - rw * W);
-      const long long ff = rw / S;
-      c_frame[e] = (int)ff;
-      c_rc[e] = (int)(rw - ff * S) * C + ww * 64 + 16 * (tt & 3) + (int)(code & 15);
+      // the block lies in one frame (launch condition (S * W) % 64 == 0): every item's frame is this thread's f, so
+      // no 64-bit division by S per item
+      c_frame[e] = (int)f;
+      c_rc[e] = (int)(rw - f * S) * C + ww * 64 + 16 * (tt & 3) + (int)(code & 15);
       c_amask[e] = PACK ? code >> 12 : pam[k];
     }
   }
