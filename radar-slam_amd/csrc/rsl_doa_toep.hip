@@ -732,9 +732,16 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
     }
   }
 #endif
-  const size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);
+  size_t lds = (size_t)ntiles * KB * 2 * 64 * sizeof(uint4);
   if (lds > 64 * 1024) return hipErrorInvalidValue;  // caller checks toep_table_fits()
   (void)max_blocks;
+#ifdef RSL_DEV_KNOBS
+  // RSL_DOA_WGPC: at most this many workgroups per CU (extra dynamic LDS), i.e. waves per SIMD (occupancy study)
+  if (const char* e = getenv("RSL_DOA_WGPC")) {
+    const int w = atoi(e);
+    if (w > 0 && (size_t)(160 * 1024) / w > lds) lds = (size_t)(160 * 1024) / w - 256;
+  }
+#endif
   // Grid sized from the cell count (the capacity when the count is on the device; blocks past the cells exit before
   // loading the table) with ~8 passes per wave, instead of a persistent grid of resident blocks: measured 1.52-1.56
   // vs 1.71-1.79 ms per 1000 cfg2 frames (4 or 16 passes per wave: no better, tools/ppw_ab.sh).
