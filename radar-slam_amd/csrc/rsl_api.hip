@@ -226,8 +226,8 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   bool sup = true;
   int group = 1;
   hipError_t e;
-  // packed range spectra between K1 and K2 (6 B per value; the per-bin exponents after the packed tiles, inside the
-  // c64-sized work buffer the caller provides)
+  // packed range spectra between K1 and K2 (6 B per value, each bin's exponent inside its 48-B unit; the tiles fill
+  // the first 3/4 of the c64-sized work buffer the caller provides; wexp is the launchers' packed-path switch)
   unsigned char* wexp =
       rsl::work_packed_supported(C, S) ? (unsigned char*)work + (size_t)F * A * C * S * 6 : nullptr;
   {

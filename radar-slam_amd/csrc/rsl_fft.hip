@@ -63,13 +63,16 @@ RSL_DEV void st8(float2* p, float2 x) {
 
 // Packed `work` (K1 -> K2 at S = 512, C = 128).  Per K1 tile (frame, antenna, 8-chirp block cb)
 // a 24 KiB block of 6 planes x 256 bin pairs x 16 B: planes 0-2 hold the even bin 2p of pair p, planes 3-5 the odd
-// bin 2p + 1, each bin's 8 rows x (re, im) as 16 fields of 24 bits (12 dwords, 3 x 16 B).  Every K1 store and every K2
-// load is a 16-B access: a K1 wave stores 1 KiB runs (lane = pair), a K2 lane loads the 3 chunks of one (bin, chirp
-// block) and a wave's loads cover whole 128-B lines (16 bins = 8 pairs of one plane, or the other plane).  Each bin of a
-// tile has its own exponent e (int8, after the planes: [tile][512 bins]); a field is n = rint(v 2^(22 - e)), |n| < 2^22,
-// stored offset-binary (the low 24 bits of the f32 1.5 2^23 + n), so the value's error is <= 2^(e - 23) = two fp32 ulps
-// of the bin's largest component, fp32-class for the RDS (1e-5 max-relative tolerance) and the peak decisions.
-// 6 B per value instead of 8: K1 + K2 move 14.1 instead of 16.8 MB per cfg2 frame.
+// bin 2p + 1, each bin's 8 rows x (re, im) as 16 fields of 23 bits plus the bin's exponent (12 dwords, 3 x 16 B).
+// Every K1 store and every K2 load is a 16-B access: a K1 wave stores 1 KiB runs (lane = pair), a K2 lane loads the 3
+// chunks of one (bin, chirp block) and a wave's loads cover whole 128-B lines (16 bins = 8 pairs of one plane, or the
+// other plane).  Each bin of a tile has its own exponent e (int8); a field is n = rint(v 2^(22 - e)), |n| < 2^22, stored
+// offset-binary (the low 23 bits of the f32 1.5 2^23 + n: every such f32 has exponent 2^23), so the value's error is
+// <= 2^(e - 23) = two fp32 ulps of the bin's largest component, fp32-class for the RDS (1e-5 max-relative tolerance)
+// and the peak decisions.  The exponent byte sits in the 4 spare bits of the first two field groups (round 3; it was
+// a separate [tile][512] byte array before, 0.26 GB of extra K1 writes and K2 byte loads per 2000 frames, and the
+// fields were 24-bit with the 24th bit always 0: the same values, bit for bit).
+// 6 B per value instead of 8: K1 + K2 move 14.0 instead of 16.8 MB per cfg2 frame.
 constexpr float kPkMagic = 12582912.0f;  // 1.5 * 2^23
 constexpr int kPkPlane = 4096;           // bytes per plane of one tile (256 pairs x 16 B)
 constexpr int kPkTile = 6 * kPkPlane;    // bytes per tile
@@ -79,35 +82,42 @@ RSL_DEV int pk_exp(unsigned mbits) {
   return e < -100 ? -100 : (e > 127 ? 127 : e);
 }
 RSL_DEV float pk_pow2(int k) { return __uint_as_float((unsigned)(127 + k) << 23); }
-// 16 fields (8 complex) -> 12 dwords: groups of 4 fields u0..u3 -> u0 | u1 << 24, u1 >> 8 | u2 << 16, u2 >> 16 | u3 << 8
-RSL_DEV void pk_pack16(const float (&f)[16], float s, uint4 (&o)[3]) {
+// 16 fields (8 complex) of one bin with its exponent e -> 12 dwords: field group g (u0..u3, 23 bits each) and a nibble
+// x_g in 96 bits, u0 | u1 << 23, u1 >> 9 | u2 << 14, u2 >> 18 | u3 << 5 | x_g << 28; x_0 / x_1 = the low / high nibble
+// of the int8 e, x_2 = x_3 = 0
+RSL_DEV void pk_pack16(const float (&f)[16], int e, uint4 (&o)[3]) {
+  const float s = pk_pow2(22 - e);
   unsigned u[16], d[12];
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     // fma rounds v s to the nearest integer (|v s| < 2^22); the min keeps a value that rounds up to 2^22 in range
     const unsigned b = min(__float_as_uint(fmaf(f[c], s, kPkMagic)), 0x4B7FFFFFu);
-    u[c] = b & 0xFFFFFFu;
+    u[c] = b & 0x7FFFFFu;
   }
+  const unsigned eb = (unsigned)e & 0xFFu;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    d[3 * g] = u[4 * g] | (u[4 * g + 1] << 24);
-    d[3 * g + 1] = (u[4 * g + 1] >> 8) | (u[4 * g + 2] << 16);
-    d[3 * g + 2] = (u[4 * g + 2] >> 16) | (u[4 * g + 3] << 8);
+    const unsigned x = g == 0 ? (eb & 0xFu) : (g == 1 ? (eb >> 4) : 0u);
+    d[3 * g] = u[4 * g] | (u[4 * g + 1] << 23);
+    d[3 * g + 1] = (u[4 * g + 1] >> 9) | (u[4 * g + 2] << 14);
+    d[3 * g + 2] = (u[4 * g + 2] >> 18) | (u[4 * g + 3] << 5) | (x << 28);
   }
   o[0] = make_uint4(d[0], d[1], d[2], d[3]);
   o[1] = make_uint4(d[4], d[5], d[6], d[7]);
   o[2] = make_uint4(d[8], d[9], d[10], d[11]);
 }
-RSL_DEV void pk_unpack16(const uint4 (&w)[3], float s, float (&f)[16]) {
+RSL_DEV void pk_unpack16(const uint4 (&w)[3], float (&f)[16]) {
   const unsigned d[12] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w,
                           w[2].x, w[2].y, w[2].z, w[2].w};
+  const int e = (int)(signed char)((d[2] >> 28) | ((d[5] >> 28) << 4));
+  const float s = pk_pow2(e - 22);
   const float off = -kPkMagic * s;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const unsigned u0 = d[3 * g] & 0xFFFFFFu;
-    const unsigned u1 = __builtin_amdgcn_alignbit(d[3 * g + 1], d[3 * g], 24) & 0xFFFFFFu;
-    const unsigned u2 = __builtin_amdgcn_alignbit(d[3 * g + 2], d[3 * g + 1], 16) & 0xFFFFFFu;
-    const unsigned u3 = d[3 * g + 2] >> 8;
+    const unsigned u0 = d[3 * g] & 0x7FFFFFu;
+    const unsigned u1 = __builtin_amdgcn_alignbit(d[3 * g + 1], d[3 * g], 23) & 0x7FFFFFu;
+    const unsigned u2 = __builtin_amdgcn_alignbit(d[3 * g + 2], d[3 * g + 1], 14) & 0x7FFFFFu;
+    const unsigned u3 = (d[3 * g + 2] >> 5) & 0x7FFFFFu;
     // 0x4B000000 | u = 2^23 + u = 1.5 2^23 + n exactly; (that - 1.5 2^23) s in one rounding (exact: n s)
     f[4 * g] = fmaf(__uint_as_float(0x4B000000u | u0), s, off);
     f[4 * g + 1] = fmaf(__uint_as_float(0x4B000000u | u1), s, off);
@@ -365,6 +375,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
                                                               float2* __restrict__ work, int slot,
                                                               unsigned char* __restrict__ wexp) {
   constexpr int S = 512, CB = 8;
+  (void)wexp;  // the exponents travel inside the packed units (pk_pack16)
   __shared__ float2 ldtab[S];
   __shared__ float2 ldtw[32 * kR512TwPitch];
   __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // stage exchange; aliased by the output buffer
@@ -478,8 +489,8 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     }
     const int e0 = pk_exp(m0), e1 = pk_exp(m1);
     uint4 w0[3], w1[3];
-    pk_pack16(f0, pk_pow2(22 - e0), w0);
-    pk_pack16(f1, pk_pow2(22 - e1), w1);
+    pk_pack16(f0, e0, w0);
+    pk_pack16(f1, e1, w1);
     const size_t tile = (size_t)fa * ncb + cb;
     uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile) + tid;
 #pragma unroll
@@ -487,8 +498,6 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
       st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
       st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
     }
-    reinterpret_cast<unsigned short*>(wexp + tile * S)[tid] =
-        (unsigned short)((unsigned)(e0 & 0xFF) | ((unsigned)(e1 & 0xFF) << 8));
     if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
     __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
   };
@@ -882,6 +891,7 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
   // a runtime 32-bit division (≈ 200 SALU per wave before)
   constexpr int C = 128, S = 512, NT = 16 * KB, NR = KB + 2, NCB = 16;
   (void)S_arg;
+  (void)wexp;  // the exponents travel inside the packed units (pk_unpack16)
   static_assert(KB == 16 || KB == 32, "one unit (bin, class) per thread; the halo from threads 0-31");
   // rows of C + 1 float2, columns unpadded (the stage-2 row writes of 16-lane groups hit 16 distinct banks); the
   // per-class exchange pitch 8 NR + 1 (the halo threads' writes, one class per lane, hit distinct banks).  19 KB of
@@ -897,7 +907,7 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
   constexpr unsigned nkb = (unsigned)(S / KB);
   const unsigned g = (unsigned)xcd_tile(blockIdx.x, gridDim.x);  // TPW consecutive tiles g TPW + i per workgroup
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
-  auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3], int& e) {
+  auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3]) {
     const uint4* src =
         reinterpret_cast<const uint4*>(wb + (tile0 + cls) * kPkTile + (size_t)(3 * (k & 1)) * kPkPlane) + (k >> 1);
 #pragma unroll
@@ -907,7 +917,6 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
       else
         w[jj] = src[jj * (kPkPlane / 16)];
     }
-    e = DBG == 6 ? (k & 7) : (int)(signed char)wexp[(tile0 + cls) * (size_t)S + k];
   };
   const int b = tid % KB, cls = tid / KB;
   const bool halo = tid < 2 * NCB;  // threads 0-31: (side, class) = (tid / 16, tid % 16)
@@ -915,28 +924,26 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
   // every tile's loads issued before the first tile's transform (TPW > 1: the later tiles' loads are in flight
   // during the earlier tiles' transforms and stores)
   uint4 wi[TPW][3], wh[TPW][3];
-  int ei[TPW], eh[TPW];
 #pragma unroll
   for (int q = 0; q < TPW; ++q) {
     const unsigned tile = g * TPW + q;
     const int k0 = (int)(tile % nkb) * KB;
     const size_t tile0 = (size_t)(tile / nkb) * NCB;
-    unit(tile0, k0 + b, cls, wi[q], ei[q]);
-    eh[q] = 0;
+    unit(tile0, k0 + b, cls, wi[q]);
     if (halo) {
       int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
       kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
-      unit(tile0, kk, hcls, wh[q], eh[q]);
+      unit(tile0, kk, hcls, wh[q]);
     }
   }
   if constexpr (DBG == 7) {
-    if (__uint_as_float(wi[0][0].x ^ wh[0][1].y) == 1.2345e30f) rds[tid] = make_float2((float)ei[0], (float)eh[0]);
+    if (__uint_as_float(wi[0][0].x ^ wh[0][1].y) == 1.2345e30f) rds[tid] = make_float2((float)wi[0][1].z, 0.f);
     return;
   }
   // one unit (K1 stored Y'_c[k1] = W128^(c k1) DFT8_r already): decode, write xb[c][k1][b2]
-  auto stage1 = [&](const uint4(&w)[3], int e, int c, int b2) {
+  auto stage1 = [&](const uint4(&w)[3], int c, int b2) {
     float f[16];
-    pk_unpack16(w, pk_pow2(e - 22), f);
+    pk_unpack16(w, f);
     float2* dst = xb + c * XP + b2;
 #pragma unroll
     for (int k = 0; k < 8; ++k) dst[k * NR] = make_float2(f[2 * k], f[2 * k + 1]);
@@ -949,8 +956,8 @@ __global__ __launch_bounds__(16 * KB) void k_doppler_detect_r128(const float2* _
     const int k0 = (int)(tile % nkb) * KB;
     const unsigned fa = tile / nkb;
     if (q > 0) __syncthreads();  // the previous tile's body is done with the LDS tile
-    stage1(wi[q], ei[q], cls, b + 1);
-    if (halo) stage1(wh[q], eh[q], hcls, hside ? NR - 1 : 0);
+    stage1(wi[q], cls, b + 1);
+    if (halo) stage1(wh[q], hcls, hside ? NR - 1 : 0);
     __syncthreads();
     // stage 2: DFT16 over the classes
     float2 x[16];

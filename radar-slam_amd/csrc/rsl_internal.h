@@ -31,8 +31,9 @@ hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int 
                                  float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask,
                                  int* row_count, float* dbmap, float* pk_pow, bool* supported, int* pk_group,
                                  const unsigned char* wexp = nullptr);
-// wexp non-null (both launches): `work` holds packed rows (rsl_fft.hip pk_pack16: 6 B per value in 24 KiB tiles, the
-// int8 per-bin exponents at wexp = work + F A C S 6 bytes) -- only where work_packed_supported(C, S).
+// wexp non-null (both launches): `work` holds packed rows (rsl_fft.hip pk_pack16: 6 B per value in 24 KiB tiles, each
+// bin's int8 exponent inside its 48-B unit; the pointer is only the switch, nothing is stored there) -- only where
+// work_packed_supported(C, S).
 bool work_packed_supported(int C, int S);
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,

@@ -50,8 +50,9 @@ def test_scheduling_invariance(ctx, name):
     ref = _run(ctx, ch, cube)
     assert ref[1].abs().amax().item() > 0
     what = ('work', 'rds', 'mask', 'row_count', 'peak_pow')
-    # packed `work` (S = 512, C = 128) puts the exponents after all F frames' tiles, so a frame's slice of the buffer
-    # is laid out differently in a one-frame launch: compare the outputs there, the whole buffer on repeated launches
+    # packed `work` (S = 512, C = 128) holds 3 MiB of tiles per frame from the buffer start, so a frame's c64-sized
+    # slice (4 MiB per frame) is laid out differently in a one-frame launch: compare the outputs there, the whole buffer
+    # on repeated launches
     packed = (S, C) == (512, 128)
     for f in range(F):  # one launch per frame: other grids, other tile -> workgroup maps
         got = _run(ctx, ch, cube, slice(f, f + 1))
