@@ -324,72 +324,322 @@ def cu_masked_stream(dev, ncu, side, total=256):
     return torch.cuda.ExternalStream(st.value, device=dev)
 
 
-def run_spectrum(args, world, rank, local, dev):
-    """configs[1]: 8ch x 128chirp x 512 cube, 1000 frames per step, range-Doppler FFT + peaks + the MUSIC spectrum
-    of every unique cell (f32, cell-blocked [cells / 32, 361, 32]; the reference keeps spectrum f64[G] per target,
-    angle_estimation.py:299).  One chain, no pipelining; the spectrum store dominates (51 MB per frame)."""
+def _sync_max(elapsed, dev):
+    """The max over ranks of a host-timed interval (barrier + synchronize on both sides are the caller's)."""
+    if not DIST:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def measure_spectrum(ctx, dev, F, steps, warmup, rank, world, timing=True, collective=True):
+    """configs[1]: 8ch x 128chirp x 512 cube, F frames per step, range-Doppler FFT + peaks + the MUSIC spectrum of every
+    unique cell (f32, cell-blocked [cells / 32, 361, 32]; the reference keeps spectrum f64[G] per target,
+    angle_estimation.py:299).  One chain, no pipelining; the spectrum store dominates (51 MB per frame).  Returns a
+    dict: frames/s, per-step time, the spectrum scan's HBM roofline and the FFT stage's."""
     import torch
     import torch.distributed as dist
     import rsl
     A, C, S, Tc = 8, 128, 512, 51.2e-6
-    F = args.frames_per_step or 1000
     cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, spectrum=True, cell_frac=0.6)
-    ctx = rsl.get_context(local)
     ch = rsl.RadarChain(cfg, F, ctx)
     cubes = make_cubes(ctx, 2, F, A, C, Tc, rank)
 
     def step(i):
         ch.run(cubes[i % 2], esprit=False, velocity=False)
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
     ne, nc = ch.totals()
     if ne > ch.entry_cap or nc > ch.cell_cap:
         raise RuntimeError('peak capacity exceeded')
-    if not args.no_timing:
+    if timing:
         ctx.timing(True)
         ctx.timing_reset()
-    if DIST:
+    if DIST and collective:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         step(i)
     torch.cuda.synchronize()
-    if DIST:
+    if DIST and collective:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if DIST:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    kt = ctx.timing_read() if not args.no_timing else {}
+    if collective:
+        elapsed = _sync_max(elapsed, dev)
+    kt = ctx.timing_read() if timing else {}
     ctx.timing(False)
-    if rank != 0:
-        return
     G = len(ch.grid)
-    line = {"metric": "radar frames/sec, range-Doppler FFT + MUSIC spectrum (configs[1]), 8ch x 128chirp x 512",
-            "value": F * args.steps * world / elapsed, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "configs[1]: 8ch x 128chirp x 512 synthetic cube, RDS + peaks + MUSIC spectrum of "
-                                   "every unique cell (f32, cell-blocked [cells/32, 361, 32])", "frames_per_step": F,
-                       "doa_grid": G, "parallelism": f"frame-sharded x{world}"},
-            "peaks_per_frame": ne / F, "cells_per_frame": nc / F}
+    out = {"value": F * steps * (world if collective else 1) / elapsed, "unit": "frames/s",
+           "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup, "frames_per_step": F,
+           "peaks_per_frame": ne / F, "cells_per_frame": nc / F, "doa_grid": G}
     if kt:
         per = lambda k: kt[k][0] / max(kt[k][1], 1)
         sbytes = nc * G * 4 + nc * A * 8  # spectrum store + signature gather
         t = per('doa_scan') * 1e-3
-        line["roofline"] = {"bound": "hbm", "kernel": "k_doa_toep (spectrum, Toeplitz f16 MFMA)", "achieved": sbytes / t / 1e9,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sbytes / t / 1e9 / HBM_PEAK_GBS,
-                            "traffic": spectrum_traffic(F), "avg_launch_ms": per('doa_scan'),
-                            "algorithmic_bytes_per_launch": sbytes}
+        out["roofline"] = {"bound": "hbm", "kernel": "k_doa_toep (spectrum, Toeplitz f16 MFMA)",
+                           "achieved": sbytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": sbytes / t / 1e9 / HBM_PEAK_GBS, "traffic": spectrum_traffic(F),
+                           "traffic_source": 'PMC FETCH_SIZE x 2 + WRITE_SIZE from ' + os.path.relpath(SPEC_PROFILE, ROOT),
+                           "avg_launch_ms": per('doa_scan'), "algorithmic_bytes_per_launch": sbytes}
         fb = 2 * A * C * S * 8 * F
         tf = (per('range_fft') + per('doppler_fft')) * 1e-3
-        line["fft_stage"] = {"bound": "hbm", "achieved": fb / tf / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": fb / tf / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fb}
-        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) for k, v in kt.items() if v[1]}
+        out["fft_stage"] = {"bound": "hbm", "achieved": fb / tf / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": fb / tf / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fb}
+        out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) for k, v in kt.items() if v[1]}
+    del ch, cubes
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_spectrum(args, world, rank, local, dev):
+    """`--config spectrum`: configs[1] as its own JSON line (measure_spectrum)."""
+    import rsl
+    ctx = rsl.get_context(local)
+    F = args.frames_per_step or 1000
+    r = measure_spectrum(ctx, dev, F, args.steps, args.warmup, rank, world, timing=not args.no_timing)
+    if rank != 0:
+        return
+    line = {"metric": "radar frames/sec, range-Doppler FFT + MUSIC spectrum (configs[1]), 8ch x 128chirp x 512",
+            "value": r.pop("value"), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": r.pop("ms_per_step"), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "configs[1]: 8ch x 128chirp x 512 synthetic cube, RDS + peaks + MUSIC spectrum of "
+                                   "every unique cell (f32, cell-blocked [cells/32, 361, 32])", "frames_per_step": F,
+                       "doa_grid": r["doa_grid"], "parallelism": f"frame-sharded x{world}"}}
+    line.update({k: v for k, v in r.items() if k not in ("steps", "warmup", "frames_per_step", "unit")})
     print(json.dumps(line), flush=True)
+
+
+def kernel_bytes_k1k2(A, C, S, F):
+    """Design bytes per launch of K1 / K2 (the work round trip included: kernel efficiencies, not the stage roofline).
+    Packed `work` at cfg2 (rsl_fft.hip pk_pack16: 6 B per value, the bin's exponent inside its 48-B unit):
+      K1 k_range_fft_r512: read the c64 cube (8 B per value) + write the packed range spectra (6 B)  = A C S 14 B/frame
+      K2 k_doppler_detect_r128: read the packed spectra of 16 + 2 halo range bins per 16-bin tile + write the c64 RDS
+         (masks / peak powers, ~1 %, not counted)                                     = A C S (6 x 18 / 16 + 8) B/frame
+    c64 `work` at other shapes (k_range_fft_p / k_doppler_detect): 2 A C S 8 B per frame each."""
+    if (C, S) == (128, 512):
+        return {'range_fft': A * C * S * 14.0 * F, 'doppler_fft': A * C * S * (6.0 * 18 / 16 + 8) * F}
+    return {'range_fft': 2 * A * C * S * 8 * F, 'doppler_fft': 2 * A * C * S * 8 * F}
+
+
+def chain_traffic_per_frame():
+    """Whole-chain HBM bytes per frame from the committed PMC profile (every rsl:: kernel of the timed chain: K1, K2,
+    offsets, compaction, DoA, velocity, trajectory; the synthesis is not in the timed region), or None."""
+    try:
+        prof = json.load(open(PROFILE))
+    except (OSError, ValueError):
+        return None
+    tot = sum(e.get('hbm_bytes', 0.0) for name, e in prof.get('kernels', {}).items()
+              if name.startswith('rsl::') and not name.startswith('rsl::k_synth'))
+    return tot / prof.get('frames_per_launch', 1000)
+
+
+def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.01, pipeline=True, streams=1,
+                  timing=True, standalone=True, collective=True):
+    """The full chain (RDS + peaks + MUSIC argmax + ESPRIT + LS velocity + trajectory) on batches of F frames already
+    resident in HBM: `steps` timed steps after `warmup`, bracketed by barrier + synchronize (max over ranks when
+    `collective`).  Returns elapsed seconds, per-kernel timings (live and standalone), totals and the chain."""
+    import torch
+    import torch.distributed as dist
+    import rsl
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=ridge)
+    NS = max(1, streams)
+    if F % NS:
+        raise SystemExit('--frames-per-step must be a multiple of --streams')
+    nb = 2
+    cubes = make_cubes(ctx, nb, F, A, C, cfg.chirp_duration, rank)
+    # trajectory reduction (SURVEY §8e): device prefix scan of this rank's frame block, all-gather of the
+    # 16-double block summaries and of the per-frame poses over RCCL/xGMI (rsl/traj.py)
+    reducer = rsl.TrajectoryReducer(ctx, F, dt=cfg.dt, collective=collective)
+    main = torch.cuda.current_stream(dev)
+    if pipeline:
+        NS = 1
+        vel2 = torch.empty((2, F, 8), dtype=torch.float64, device=dev)
+        chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
+        sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        cum = os.environ.get('RSL_BENCH_CUMASK')  # "front:back" CU counts: the two halves on CU-masked streams
+        if cum:
+            nf, nbk = (int(x) for x in cum.split(':'))
+            sA, sB = cu_masked_stream(dev, nf, 0), cu_masked_stream(dev, nbk, 1)
+        evA = [torch.cuda.Event() for _ in range(2)]
+        evB = [torch.cuda.Event() for _ in range(2)]
+        # the trajectory (scan, RCCL summary all-gather, pose gather to rank 0, smoothing) on a third stream, so the
+        # collectives' latency stays off the back stream: batch i + 1's DoA does not wait for batch i's gather
+        sC = torch.cuda.Stream(dev) if os.environ.get('RSL_BENCH_TRAJ_STREAM', '1') != '0' else None
+        evC = [torch.cuda.Event() for _ in range(2)]
+        used = [False, False]
+    else:
+        vel = torch.empty((F, 8), dtype=torch.float64, device=dev)
+        chains = [rsl.RadarChain(cfg, F // NS, ctx, vel_out=vel[k * (F // NS):(k + 1) * (F // NS)]) for k in range(NS)]
+        streams = [torch.cuda.Stream(dev) for _ in range(NS)]
+    # 0: offsets + compaction on the front stream; 1: compaction on the back stream; 2: both on the back stream
+    EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '1'))
+
+    def step_pipelined(i):
+        k = i % 2
+        ch = chains[k]
+        sA.wait_stream(main)
+        with torch.cuda.stream(sA):
+            if used[k]:
+                sA.wait_event(evB[k])  # batch i-2's back half is done with these buffers
+            ch.run_front(cubes[i % nb], emit=EMIT_BACK == 0, offsets=EMIT_BACK < 2)
+            evA[k].record(sA)
+        with torch.cuda.stream(sB):
+            sB.wait_event(evA[k])
+            if sC is not None and used[k]:
+                sB.wait_event(evC[k])  # batch i-2's trajectory step has read chain k's velocities
+            ch.run_back(emit=EMIT_BACK > 0, offsets=EMIT_BACK == 2)
+            if sC is None:
+                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
+            evB[k].record(sB)
+        if sC is not None:
+            with torch.cuda.stream(sC):
+                sC.wait_event(evB[k])
+                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
+                evC[k].record(sC)
+        used[k] = True
+
+    def step(i):
+        if pipeline:
+            return step_pipelined(i)
+        cube = cubes[i % nb]
+        for k, (ch, st) in enumerate(zip(chains, streams)):  # independent frame slices, concurrent streams
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                ch.run(cube[k * (F // NS):(k + 1) * (F // NS)])
+        for st in streams:
+            main.wait_stream(st)
+        reducer.step(vel, vstride=vel.shape[1], nv=2)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    for ch in (chains[:min(warmup, 2)] if pipeline else chains):  # the chains that ran (pipelined: one per step)
+        ne, nc = ch.totals()
+        if ne > ch.entry_cap or nc > ch.cell_cap:
+            raise RuntimeError('peak capacity exceeded')
+    if timing:
+        ctx.timing(True)
+        ctx.timing_reset()
+    if DIST and collective:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    if DIST and collective:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if collective:
+        elapsed = _sync_max(elapsed, dev)
+    kt = ctx.timing_read() if timing else {}
+    ks = {}  # standalone kernel times: the pipelined timed region overlaps the two halves of consecutive batches
+    if kt and pipeline and standalone:
+        ctx.timing_reset()
+        for i in range(STANDALONE_RUNS):  # one chain at a time on one stream; per-kernel means over these runs
+            chains[0].run(cubes[i % nb])
+        torch.cuda.synchronize()
+        ks = ctx.timing_read()
+    ctx.timing(False)
+    counted = chains[:1] if pipeline else chains  # pipelined: both buffers hold a full batch
+    ne = sum(ch.totals()[0] for ch in counted)
+    nc = sum(ch.totals()[1] for ch in counted)
+    return dict(elapsed=elapsed, kt=kt, ks=ks, ne=ne, nc=nc, NS=NS, G=len(chains[0].grid), cubes=cubes,
+                chains=chains, reducer=reducer)
+
+
+def chain_rooflines(r, A, C, S, F, config):
+    """roofline (FFT stage, live), fft_stage_standalone, roofline_doa, kernel_rooflines_standalone and the per-kernel
+    ms of one measure_chain result."""
+    kt, ks, NS, G = r['kt'], r['ks'], r['NS'], r['G']
+    out = {}
+    if not kt:
+        return out
+    per = lambda name: kt[name][0] / max(kt[name][1], 1)  # ms per launch
+    Fl = F // NS
+    ncl = r['nc'] / NS  # unique cells per launch
+    # Algorithmic work per launch (SURVEY §8d):
+    #  FFT stage (K1 + K2): read the c64 cube + write the c64 RDS, counted once: 2 A C S 8 B per frame
+    #  K5 k_doa_toep: one real dot product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2),
+    #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
+    src_std = ks if ks else kt
+    packed = (C, S) == (128, 512)
+    fft_names = ({'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'} if packed
+                 else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
+    per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
+    flops = 3 * 2 * (2 * A - 1) * ncl * G
+    kbytes = kernel_bytes_k1k2(A, C, S, Fl)
+
+    def entry(name, ms):
+        if name == 'doa_scan':
+            ach = flops / (ms * 1e-3) / 1e12
+            return {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                    "traffic": pmc_traffic('k_doa_toep', Fl, config), "traffic_source": TRAFFIC_SOURCE,
+                    "avg_launch_ms": ms, "algorithmic_flops_per_launch": flops,
+                    "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
+        kern = fft_names[name]
+        ach = kbytes[name] / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, config),
+                "traffic_source": TRAFFIC_SOURCE, "avg_launch_ms": ms, "design_bytes_per_launch": kbytes[name],
+                "note": "per-kernel design bytes (cube or work in, work or RDS out): the work round trip counts "
+                        "here, so these fractions are kernel efficiencies, not the stage's algorithmic roofline"}
+
+    # Headline roofline = the FFT stage (SURVEY §8(d)): its algorithmic bytes counted ONCE per frame over the summed
+    # average launch durations of the kernels that implement it (K1 range FFT + K2 Doppler FFT / fftshift / detection),
+    # measured live by hipEvents on their stream over the timed region; traffic = the same kernels' PMC HBM bytes per
+    # launch.  The `work` intermediate between K1 and K2 is NOT algorithmic: it shows up as traffic above the
+    # algorithmic bytes.
+    big = ('range_fft', 'doppler_fft', 'doa_scan')
+    fft_k = [k for k in ('range_fft', 'doppler_fft') if k in kt and kt[k][1]]
+    fft_bytes = 2 * A * C * S * 8 * Fl
+
+    def stage(src, timed):
+        t = sum(src[k][0] / max(src[k][1], 1) for k in fft_k) * 1e-3
+        tr = [pmc_traffic(fft_names[k], Fl, config) for k in fft_k]
+        return {"bound": "hbm", "kernels": [fft_names[k] for k in fft_k],
+                "achieved": fft_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": fft_bytes / t / 1e9 / HBM_PEAK_GBS,
+                "traffic": None if any(x is None for x in tr) else sum(tr), "traffic_source": TRAFFIC_SOURCE,
+                "avg_launch_ms": t * 1e3, "algorithmic_bytes_per_launch": fft_bytes, "timed": timed}
+
+    out["roofline"] = stage(kt, "hipEvents over the timed region (pipelined: the stage co-runs with the previous "
+                                "batch's DoA scan)" if ks else "hipEvents over the timed region")
+    if ks:
+        out["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
+    out["roofline_doa"] = entry('doa_scan', per('doa_scan'))
+    out["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big if k in src_std}
+    out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
+    if ks:
+        out["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
+    return out
+
+
+def configs_4_frame(ctx, dev, F=100, steps=4, warmup=2):
+    """Bounded sub-measurement of the configs[4] frame shape (A16 C256 S1024, the 1 M-frame 8-GPU workload's frame) on
+    this GPU: the same full chain, pipelined, F frames per step, this rank only (no collective)."""
+    import torch
+    A, C, S, Tc = 16, 256, 1024, 102.4e-6
+    r = measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, 0, 1, standalone=True, collective=False)
+    out = {"what": "configs[4] frame shape (16ch x 256chirp x 1024), full chain pipelined, one GPU, "
+                   f"{F} frames per step, {steps} timed steps", "value": F * steps / r['elapsed'],
+           "unit": "frames/s", "ms_per_step": r['elapsed'] / steps * 1e3, "frames_per_step": F,
+           "peaks_per_frame": r['ne'] / F, "cells_per_frame": r['nc'] / F,
+           "projected_1M_frames_8_gpus_s": 1e6 / 8 / (F * steps / r['elapsed'])}
+    rf = chain_rooflines(r, A, C, S, F, 'cfg5')
+    for k in ('roofline', 'fft_stage_standalone', 'roofline_doa', 'kernel_ms_standalone'):
+        if k in rf:
+            out[k] = rf[k]
+    del r
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -406,6 +656,8 @@ def main():
                          'measurements, not the metric line')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-pcie', action='store_true', help='skip the PCIe-inclusive side measurement')
+    ap.add_argument('--no-extra', action='store_true',
+                    help='skip the configs[1] / configs[4]-frame sub-measurements of the default cfg2 line')
     ap.add_argument('--cpu-peaks', type=int, default=3000,
                     help='peaks per frame through the loop-faithful CPU DoA (the bounded sample; <= 0: every peak)')
     ap.add_argument('--cpu-procs', type=int, default=0,
@@ -418,7 +670,7 @@ def main():
                     help='concurrent HIP streams per GPU; each runs the chain on F/streams frames of the step')
     ap.add_argument('--pipeline', type=int, default=int(os.environ.get('RSL_BENCH_PIPELINE', '1')),
                     help='1: double-buffered chains on two streams; batch i+1\'s memory-bound front half (RDS, '
-                         'detection, compaction) runs concurrently with batch i\'s compute-bound back half (DoA, '
+                         'detection, offsets) runs concurrently with batch i\'s back half (compaction, DoA, '
                          'velocity, trajectory)')
     args = ap.parse_args()
 
@@ -450,125 +702,17 @@ def main():
         A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 100
     else:
         A, C, S, Tc, F = 8, 128, 512, 51.2e-6, args.frames_per_step or 2000  # 5 steps = configs[2]'s 10 k frames
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=args.ridge)
     ctx = rsl.get_context(local)
-    NS = max(1, args.streams)
-    if F % NS:
-        raise SystemExit('--frames-per-step must be a multiple of --streams')
-    vel = torch.empty((F, 8), dtype=torch.float64, device=dev)
-    chains = [rsl.RadarChain(cfg, F // NS, ctx, vel_out=vel[k * (F // NS):(k + 1) * (F // NS)]) for k in range(NS)]
-    chain = chains[0]
-    streams = [torch.cuda.Stream(dev) for _ in range(NS)]
-    nb = 2
-    cubes = make_cubes(ctx, nb, F, A, C, cfg.chirp_duration, rank)
-    # trajectory reduction: device prefix scan of this rank's frame block, all-gather of the
-    # 16-double block summaries and of the per-frame poses over RCCL/xGMI (rsl/traj.py)
-    reducer = rsl.TrajectoryReducer(ctx, F, dt=cfg.dt)
-
-    main = torch.cuda.current_stream(dev)
-
-    if args.pipeline:
-        NS = 1
-        vel2 = torch.empty((2, F, 8), dtype=torch.float64, device=dev)
-        chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
-        chain = chains[0]
-        sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-        cum = os.environ.get('RSL_BENCH_CUMASK')  # "front:back" CU counts: the two halves on CU-masked streams
-        if cum:
-            nf, nbk = (int(x) for x in cum.split(':'))
-            sA, sB = cu_masked_stream(dev, nf, 0), cu_masked_stream(dev, nbk, 1)
-        evA = [torch.cuda.Event() for _ in range(2)]
-        evB = [torch.cuda.Event() for _ in range(2)]
-        # the trajectory (scan, RCCL summary all-gather, pose gather to rank 0, smoothing) on a third stream, so the
-        # collectives' latency stays off the back stream: batch i + 1's DoA does not wait for batch i's gather
-        sC = torch.cuda.Stream(dev) if os.environ.get('RSL_BENCH_TRAJ_STREAM', '1') != '0' else None
-        evC = [torch.cuda.Event() for _ in range(2)]
-        used = [False, False]
-
-    # 0: offsets + compaction on the front stream; 1: compaction on the back stream; 2: both on the back stream
-    EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '1'))
-
-    def step_pipelined(i):
-        k = i % 2
-        ch = chains[k]
-        sA.wait_stream(main)
-        with torch.cuda.stream(sA):
-            if used[k]:
-                sA.wait_event(evB[k])  # batch i-2's back half is done with these buffers
-            ch.run_front(cubes[i % nb], emit=EMIT_BACK == 0, offsets=EMIT_BACK < 2)
-            evA[k].record(sA)
-        with torch.cuda.stream(sB):
-            sB.wait_event(evA[k])
-            if sC is not None and used[k]:
-                sB.wait_event(evC[k])  # batch i-2's trajectory step has read chain k's velocities
-            ch.run_back(emit=EMIT_BACK > 0, offsets=EMIT_BACK == 2)
-            if sC is None:
-                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
-            evB[k].record(sB)
-        if sC is not None:
-            with torch.cuda.stream(sC):
-                sC.wait_event(evB[k])
-                reducer.step(ch.vel, vstride=ch.vel.shape[1], nv=2)
-                evC[k].record(sC)
-        used[k] = True
-
-    def step(i):
-        if args.pipeline:
-            return step_pipelined(i)
-        cube = cubes[i % nb]
-        for k, (ch, st) in enumerate(zip(chains, streams)):  # independent frame slices, concurrent streams
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
-                ch.run(cube[k * (F // NS):(k + 1) * (F // NS)])
-        for st in streams:
-            main.wait_stream(st)
-        reducer.step(vel, vstride=vel.shape[1], nv=2)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    for ch in chains:
-        ne, nc = ch.totals()
-        if ne > ch.entry_cap or nc > ch.cell_cap:
-            raise RuntimeError('peak capacity exceeded')
-    if not args.no_timing:
-        ctx.timing(True)
-        ctx.timing_reset()
-    if DIST:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if DIST:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if DIST:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    kt = ctx.timing_read() if not args.no_timing else {}
-    ks = {}  # standalone kernel times: the pipelined timed region overlaps the two halves of consecutive batches
-    if kt and args.pipeline:
-        ctx.timing_reset()
-        for i in range(STANDALONE_RUNS):  # one chain at a time on one stream; per-kernel means over these runs
-            chains[0].run(cubes[i % nb])
-        torch.cuda.synchronize()
-        ks = ctx.timing_read()
-    ctx.timing(False)
-    counted = chains[:1] if args.pipeline else chains  # pipelined: both buffers hold a full batch
-    ne = sum(ch.totals()[0] for ch in counted)
-    nc = sum(ch.totals()[1] for ch in counted)
+    r = measure_chain(ctx, dev, A, C, Tc, F, args.steps, args.warmup, rank, world, ridge=args.ridge,
+                      pipeline=bool(args.pipeline), streams=args.streams, timing=not args.no_timing)
+    elapsed, ne, nc, NS = r['elapsed'], r['ne'], r['nc'], r['NS']
     frames_total = F * args.steps * world
     fps = frames_total / elapsed
-
     if rank != 0:
         if DIST:
             dist.destroy_process_group()
         return
-    G = len(chain.grid)
+    G = r['G']
     line = {
         "metric": METRIC, "value": fps, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -585,74 +729,27 @@ def main():
                    "pipelined": bool(args.pipeline), "parallelism": f"frame-sharded x{world}"},
         "peaks_per_frame": ne / F, "cells_per_frame": nc / F,
     }
-    if kt:
-        # per-launch figures: each kernel runs once per stream per step on F / NS frames
-        per = lambda name: kt[name][0] / max(kt[name][1], 1)  # ms per launch
-        Fl = F // NS
-        ncl = nc / NS                                          # unique cells per launch
-        # Roofline entries of the three big kernels.  Algorithmic work per launch (per kernel):
-        #  K1 (k_range_fft_r512 at cfg2): read the c64 cube (8 B per value) + write the packed range spectra (6 B
-        #     per value + one exponent byte per 8 values)                                 = A C S 14.125 bytes per frame
-        #  K2 (k_doppler_detect_r128): read the packed spectra of 16 + 2 halo range bins per 16-bin tile + write the
-        #     c64 RDS (masks / peak powers, ~1 %, not counted)                 = A C S (6.125 x 18 / 16 + 8) per frame
-        #  (c64 `work` at other shapes: k_range_fft_p / k_doppler_detect, 2 A C S 8 bytes per frame each)
-        #  K5 k_doa_toep: one real dot product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2),
-        #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
-        src_std = ks if ks else kt
-        packed = (C, S) == (128, 512)
-        # the kernels implementing K1 / K2 for this shape: packed `work` at cfg2 (rsl_fft.hip work_packed_supported)
-        fft_names = ({'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'} if packed
-                     else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
-        per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
-        flops = 3 * 2 * (2 * A - 1) * ncl * G
-        kbytes = ({'range_fft': A * C * S * 14.125 * Fl, 'doppler_fft': A * C * S * (6.125 * 18 / 16 + 8) * Fl}
-                  if packed else {'range_fft': 2 * A * C * S * 8 * Fl, 'doppler_fft': 2 * A * C * S * 8 * Fl})
-
-        def entry(name, ms):
-            if name == 'doa_scan':
-                ach = flops / (ms * 1e-3) / 1e12
-                return {"bound": "mfma", "kernel": "k_doa_toep", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                        "traffic": pmc_traffic('k_doa_toep', Fl, args.config), "traffic_source": TRAFFIC_SOURCE,
-                        "avg_launch_ms": ms,
-                        "algorithmic_flops_per_launch": flops,
-                        "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
-            kern = fft_names[name]
-            ach = kbytes[name] / (ms * 1e-3) / 1e9
-            return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, args.config),
-                    "traffic_source": TRAFFIC_SOURCE, "avg_launch_ms": ms,
-                    "design_bytes_per_launch": kbytes[name],
-                    "note": "per-kernel design bytes (cube or work in, work or RDS out): the work round trip counts "
-                            "here, so these fractions are kernel efficiencies, not the stage's algorithmic roofline"}
-
-        # Headline roofline = the FFT stage: its algorithmic bytes are counted ONCE per frame (read
-        # the c64 cube + write the c64 RDS, 2 A C S 8 B), over the summed average launch durations of the kernels
-        # that implement it (K1 range FFT + K2 Doppler FFT / fftshift / detection), measured live by hipEvents on
-        # their stream over the timed region; traffic = the same kernels' PMC HBM bytes per launch.  The `work`
-        # intermediate between K1 and K2 is NOT algorithmic: it shows up as traffic above the algorithmic bytes.
-        big = ('range_fft', 'doppler_fft', 'doa_scan')
-        fft_k = [k for k in ('range_fft', 'doppler_fft') if k in kt and kt[k][1]]
-        fft_bytes = 2 * A * C * S * 8 * Fl
-
-        def stage(src, timed):
-            t = sum(src[k][0] / max(src[k][1], 1) for k in fft_k) * 1e-3
-            tr = [pmc_traffic(fft_names[k], Fl, args.config) for k in fft_k]
-            return {"bound": "hbm", "kernels": [fft_names[k] for k in fft_k],
-                    "achieved": fft_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": fft_bytes / t / 1e9 / HBM_PEAK_GBS,
-                    "traffic": None if any(x is None for x in tr) else sum(tr), "traffic_source": TRAFFIC_SOURCE,
-                    "avg_launch_ms": t * 1e3, "algorithmic_bytes_per_launch": fft_bytes, "timed": timed}
-
-        line["roofline"] = stage(kt, "hipEvents over the timed region (pipelined: the stage co-runs with the "
-                                     "previous batch's DoA scan)" if args.pipeline else "hipEvents over the timed region")
-        if ks:
-            line["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
-        line["roofline_doa"] = entry('doa_scan', per('doa_scan'))
-        line["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big}
-        line["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
-        if ks:
-            line["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
+    line.update(chain_rooflines(r, A, C, S, F, args.config))
+    if args.config == 'cfg2':
+        # whole-chain HBM traffic per frame (committed PMC profile) beside the chain's algorithmic bytes (SURVEY §8d:
+        # FFT stage 2 A C S 8 B + the DoA signature gather 8 M N_p)
+        npk = ne / F
+        line["chain_traffic_bytes_per_frame"] = chain_traffic_per_frame()
+        line["chain_algorithmic_bytes_per_frame"] = 2 * A * C * S * 8 + 8 * A * npk
+        line["chain_traffic_source"] = ('sum of every rsl:: chain kernel\'s PMC FETCH_SIZE x 2 + WRITE_SIZE in '
+                                        + os.path.relpath(PROFILE, ROOT) + ' / frames per launch')
+    del r
+    torch.cuda.empty_cache()
+    if not args.no_extra and world == 1 and args.config == 'cfg2':
+        # the other two GPU workloads of BASELINE.json, bounded (a few seconds each), as sub-objects of the metric line
+        try:
+            line["configs_1_spectrum"] = measure_spectrum(ctx, dev, 1000, 4, 1, 0, 1, collective=False)
+        except Exception as e:
+            line["configs_1_spectrum"] = {"error": repr(e)}
+        try:
+            line["configs_4_frame"] = configs_4_frame(ctx, dev)
+        except Exception as e:
+            line["configs_4_frame"] = {"error": repr(e)}
     if not args.no_pcie and world == 1 and args.config == 'cfg2':
         line["pcie_inclusive"] = pcie_inclusive(ctx, dev)
     if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed on rank 0 at N = 1 only

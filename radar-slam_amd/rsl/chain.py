@@ -59,13 +59,22 @@ class ChainConfig:
         return C_LIGHT / self.fc
 
 
+GUARD_BYTES = 256 * 1024  # sentinel pad on each side of a guarded buffer (RadarChain(guard=True))
+GUARD_FILL = 0xA5
+
+
 class RadarChain:
-    def __init__(self, cfg: ChainConfig, frames: int, ctx: Optional[Context] = None, vel_out=None):
+    def __init__(self, cfg: ChainConfig, frames: int, ctx: Optional[Context] = None, vel_out=None,
+                 guard: bool = False):
         """vel_out: optional device f64 [frames, 8] view receiving the per-frame velocity rows (lets several
-        chains on different streams fill consecutive slices of one buffer)."""
+        chains on different streams fill consecutive slices of one buffer).
+        guard: debug canary — every device buffer of the chain gets its own allocation with GUARD_BYTES of sentinel
+        bytes on both sides; guard_violations() lists the buffers whose pads were written (a store that left its own
+        buffer: tests/test_gpu_pipelined.py)."""
         self.cfg, self.F = cfg, int(frames)
         self.ctx = ctx or get_context()
         torch, ctx = self.ctx.torch, self.ctx
+        self._guards = []
         A, C, S, F = cfg.num_antennas, cfg.num_chirps, cfg.S, self.F
         self.A, self.C, self.S = A, C, S
         tab = tables.chirp_table(cfg.fc, cfg.bandwidth, cfg.chirp_duration, cfg.sampling_rate, cfg.window_type, S)
@@ -82,7 +91,7 @@ class RadarChain:
         self.method = _lib.METHOD_MUSIC if cfg.method == 'music' else _lib.METHOD_BEAMFORMING
         self.entry_cap = int(math.ceil(cfg.entry_frac * F * A * S * C)) + 64
         self.cell_cap = (int(math.ceil(cfg.cell_frac * F * S * C)) + 64 + 3) & ~3  # a multiple of 4 (16-B rows)
-        e = ctx.empty
+        e = self._guarded_empty if guard else ctx.empty
         W = (C + 63) // 64
         self.work = e((F, A, C, S), torch.complex64)
         self.rds = e((F, A, S, C), torch.complex64)
@@ -103,6 +112,26 @@ class RadarChain:
         # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
         self.fused_doa = bool(self.steer['toeplitz']) and A >= 2 and not cfg.spectrum
         self.spec = e(((self.cell_cap + 31) // 32, len(self.grid), 32), torch.float32) if cfg.spectrum else None
+
+    def _guarded_empty(self, shape, dtype):
+        torch = self.ctx.torch
+        n = 1
+        for d in (shape if isinstance(shape, tuple) else (shape,)):
+            n *= int(d)
+        nbytes = n * torch.empty((), dtype=dtype).element_size()
+        raw = torch.empty((2 * GUARD_BYTES + nbytes,), dtype=torch.uint8, device=self.ctx.device)
+        raw.fill_(GUARD_FILL)
+        self._guards.append(raw)
+        return raw[GUARD_BYTES:GUARD_BYTES + nbytes].view(dtype).view(shape)
+
+    def guard_violations(self):
+        """Indices (allocation order) and byte counts of guarded buffers whose sentinel pads changed (synchronises)."""
+        bad = []
+        for k, raw in enumerate(self._guards):
+            n = int((raw[:GUARD_BYTES] != GUARD_FILL).sum().item() + (raw[-GUARD_BYTES:] != GUARD_FILL).sum().item())
+            if n:
+                bad.append((k, n))
+        return bad
 
     def run(self, cube, *, esprit: bool = True, velocity: bool = True):
         """Launch the whole chain for cube complex64 [F, A, C, S] on the current stream (asynchronous)."""

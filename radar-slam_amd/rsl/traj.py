@@ -124,7 +124,9 @@ class TrajectoryReducer:
     ``W - 1 - W // 2`` frames of a step are emitted by the next step or by ``finalize``."""
 
     def __init__(self, ctx, frames: int, *, dt: float = 0.1, method: str = 'trapezoidal', group=None,
-                 smoothing: bool = True, smoothing_window: int = 5, keep: bool = False):
+                 smoothing: bool = True, smoothing_window: int = 5, keep: bool = False, collective: bool = True):
+        """collective=False: this rank's trajectory only, no collective even with a process group up (the bench's
+        single-rank sub-measurements)."""
         import torch
         self.ctx, self.F, self.dt = ctx, int(frames), float(dt)
         self.method = 0 if method == 'trapezoidal' else 1
@@ -138,7 +140,7 @@ class TrajectoryReducer:
         import torch.distributed as dist
         self.dist = dist
         # collectives whenever a process group is up (also at world size 1: one rank still runs the RCCL calls)
-        self.on = dist.is_available() and dist.is_initialized()
+        self.on = collective and dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.on else 1
         self.rank = dist.get_rank(group) if self.on else 0
         self.gloo = self.on and dist.get_backend(group) == 'gloo'  # gloo gathers host tensors only

@@ -2,6 +2,12 @@
 stream A overlaps batch i-1's back half on stream B, with the compaction (emit) and optionally the offsets moved to
 the back stream (RSL_BENCH_EMIT_BACK 1 / 2). Every placement must give the same lists, angles, ESPRIT, phases and
 velocities as one serial `run` of each batch: bit-identical, since only the stream a kernel runs on changes.
+
+Canary: the pipelined chains are guarded (RadarChain(guard=True): every device buffer has its own
+allocation with 256 KiB sentinel pads on both sides), and after each batch the test checks, in pipeline order, the
+range spectra (`work`, K1's output), the RDS (K2), the peak masks / row counts and then the lists, and that no
+guard pad of either chain was written.  A failure names the first stage that differs, so a K1 fault, a K2 fault and
+a foreign store into a buffer are told apart.
 """
 import numpy as np
 import pytest
@@ -19,29 +25,48 @@ def _cubes():
                           torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1 for _ in range(NB)]
 
 
-@pytest.mark.parametrize('placement', [0, 1, 2])
-def test_pipelined_matches_serial(ctx, placement):
+def first_stage_diff(ch, w):
+    """First pipeline stage whose device buffer differs from the serial run: work (K1), rds (K2), mask / row_count
+    (K2 detection); None if all equal."""
+    for name in ('work', 'rds', 'mask', 'row_count'):
+        a, b = getattr(ch, name), w[name]
+        if not torch.equal(a, b):
+            d = (a != b).nonzero()
+            return f"{name} ({d.shape[0]} values differ, first {d[:4].tolist()})"
+    return None
+
+
+def run_pipelined(ctx, cfg, cubes, placement, want, guard=True):
+    """The bench's two-stream schedule over `cubes`; returns a list of error strings (empty: bit-identical)."""
     import rsl
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)
-    cubes = _cubes()
-    ser = rsl.RadarChain(cfg, F, ctx)
-    want = []
-    for cube in cubes:
-        ser.run(cube)
-        want.append(ser.results())
-    chains = [rsl.RadarChain(cfg, F, ctx) for _ in range(2)]
+    chains = [rsl.RadarChain(cfg, F, ctx, guard=guard) for _ in range(2)]
     sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
     evA = [torch.cuda.Event() for _ in range(2)]
     evB = [torch.cuda.Event() for _ in range(2)]
     used = [False, False]
-    got = [None] * NB
+    errs = []
     main = torch.cuda.current_stream()
+
+    def check(i, ch):
+        st = first_stage_diff(ch, want[i])
+        if st:
+            errs.append(f'batch {i}: first differing stage {st}')
+        for k, c in enumerate(chains):
+            bad = c.guard_violations()
+            if bad:
+                errs.append(f'batch {i}: guard pads of chain {k} written (buffer index, bytes): {bad}')
+        res = ch.results()
+        for key, w in want[i]['res'].items():
+            if not np.array_equal(w, res[key], equal_nan=True):
+                errs.append(f'batch {i}: {key} differs')
+                break
+
     for i, cube in enumerate(cubes):
         k = i % 2
         ch = chains[k]
         if used[k]:  # buffer reuse: batch i-2's results are read before its buffers are overwritten
             evB[k].synchronize()
-            got[i - 2] = ch.results()
+            check(i - 2, ch)
         sA.wait_stream(main)
         with torch.cuda.stream(sA):
             ch.run_front(cube, emit=placement == 0, offsets=placement < 2)
@@ -53,8 +78,45 @@ def test_pipelined_matches_serial(ctx, placement):
         used[k] = True
     torch.cuda.synchronize()
     for i in (NB - 2, NB - 1):
-        got[i] = chains[i % 2].results()
-    for i in range(NB):
-        assert want[i]['c_rc'].size > 0
-        for key, w in want[i].items():
-            assert np.array_equal(w, got[i][key], equal_nan=True), f'batch {i}: {key} differs (placement {placement})'
+        check(i, chains[i % 2])
+    return errs
+
+
+def serial_reference(ctx, cfg, cubes):
+    import rsl
+    ser = rsl.RadarChain(cfg, F, ctx)
+    want = []
+    for cube in cubes:
+        ser.run(cube)
+        torch.cuda.synchronize()
+        want.append(dict(work=ser.work.clone(), rds=ser.rds.clone(), mask=ser.mask.clone(),
+                         row_count=ser.row_count.clone(), res=ser.results()))
+        assert want[-1]['res']['c_rc'].size > 0
+    return want
+
+
+@pytest.fixture(scope='module')
+def serial(ctx):
+    import rsl
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)
+    cubes = _cubes()
+    return cfg, cubes, serial_reference(ctx, cfg, cubes)
+
+
+@pytest.mark.parametrize('placement', [0, 1, 2])
+def test_pipelined_matches_serial(ctx, serial, placement):
+    cfg, cubes, want = serial
+    errs = run_pipelined(ctx, cfg, cubes, placement, want)
+    assert not errs, f'placement {placement}: ' + '; '.join(errs)
+
+
+def test_guard_canary_detects_foreign_store(ctx):
+    """The canary itself: a store one element past a guarded buffer is reported."""
+    import rsl
+    cfg = rsl.ChainConfig(num_antennas=2, num_chirps=16, chirp_duration=3.2e-6)
+    ch = rsl.RadarChain(cfg, 1, ctx, guard=True)
+    assert ch.guard_violations() == []
+    r = ch.rds.view(-1)
+    r.as_strided((1,), (1,), r.storage_offset() + r.numel()).fill_(1.0 + 1.0j)  # the 8 bytes right after the RDS
+    bad = ch.guard_violations()
+    assert len(bad) == 1 and bad[0][1] > 0
