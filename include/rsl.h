@@ -254,7 +254,8 @@ int rsl_wrapped_solve(rsl_handle h, const void* pos, const void* ang, long long 
                       int nv, int grid_n, const void* extra, int nextra, int iters, void* scratch,
                       long long scratch_bytes, void* out);
 
-/* a30, a31  the same minimisation with a basin-resolving global stage (cost <= the reference DE).
+/* a30, a31  the same minimisation with a dense multi-start global stage (a heuristic checked by cost <= the reference
+ *     DE on recorded runs; it does not guarantee that every basin of the wrapped cost is entered).
  *     Stage 1: projected 2-D Gauss-Newton in (x0, x1) = (v_x, v_y) from every point of a grid with the given spacing
  *     (a fraction of the wrap period 2 pi / k; ceil(width / spacing) points per axis, at most 32768) over
  *     [lo6[0], hi6[0]] x [lo6[1], hi6[1]], with x[2..5] held at base6 (host, clipped to the box; the regulariser's

@@ -357,7 +357,9 @@ __global__ __launch_bounds__(256) void k_wrapped_jac(const double* __restrict__ 
 // velocity box, which a coarse multi-start grid samples only in part.  Stage 1 runs a projected 2-D Gauss-Newton in
 // (x0, x1) = (v_x, v_y) -- the coordinates the data term depends on for the reference's geometry (elevation 0 and
 // p = r d make (w x p).d = 0 and d_z = 0: SURVEY §0 fact 8) -- from every point of a grid whose spacing is a fraction
-// of the wrap period, so every basin the grid resolves is entered; x[2..5] are held at base (the regulariser's
+// of the wrap period (a heuristic: the N ridge families cut cells smaller than the period, so not every basin is
+// guaranteed to be entered; the contract checked is cost <= the reference DE, tests/test_gpu_wrapped.py, and the
+// stage's latency at the reference's scale is measured there); x[2..5] are held at base (the regulariser's
 // optimum for them).  Each block keeps its best start; the best nbest blocks seed stage 2, the full nv-D Gauss-Newton
 // of k_wrapped_ms, together with the caller's extra starts.
 // ---------------------------------------------------------------------------------------------------------

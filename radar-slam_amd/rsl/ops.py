@@ -320,8 +320,11 @@ def wrapped_search(pos, ang, y, k, *, mode: int, lo, hi, nv: int = 6, w: float =
         base[2] = p[2] * 0.1 / 10.1
         base[3:] = p[3:] if nv == 6 else 0.0
     b6 = (c_double * 6)(*[float(v) for v in base])
-    # at least 64 points per axis (a smooth landscape when k is small, e.g. the pipeline's lambda = fc / c)
-    width = max(min(float(hi[0]) - float(lo[0]), float(hi[1]) - float(lo[1])), 1e-9)
+    # at least 64 points per axis (a smooth landscape when k is small, e.g. the pipeline's lambda = fc / c); the width
+    # of a collapsed axis (adaptive bounds with lo == hi) does not count: that axis gets one point (search_grid), and
+    # the other keeps its own spacing instead of a 32768-point line of starts
+    widths = [w for w in (float(hi[0]) - float(lo[0]), float(hi[1]) - float(lo[1])) if w > 1e-9]
+    width = min(widths) if widths else 1e-9
     spacing = min(float(spacing_frac) * 2 * math.pi / abs(float(k)), width / 64)
     nbytes = int(c.lib.rsl_wrapped_search_scratch_bytes(n, lo6, hi6, spacing, int(nbest), nextra))
     if nbytes < 0:

@@ -7,7 +7,8 @@ Drop-in for ``src/algorithms/advanced_velocity_optimization.py`` of the referenc
 The reference minimises the wrapped-phase cost plus piecewise penalties (:153-223) with several
 differential-evolution runs (seed 42; DE ignores the initial guess, so the runs are identical).  Here each run
 is ``rsl_wrapped_search`` mode 1: projected Gauss-Newton in (v_x, v_y) from every point of a grid whose spacing is
-half the wrap period, over the adaptive bounds (every basin of the cost is entered), then the 6-D refinement of the
+half the wrap period, over the adaptive bounds (a heuristic dense sampling of the basins, checked by the DE-cost
+tests, not a guarantee that every basin is entered), then the 6-D refinement of the
 best basins and the run's initial guess, keeping the lowest cost (see velocity_solver_improved.py for the basin
 structure).  The penalties are evaluated on the device with the reference's exact formulas.
 Parity contract: cost <= the reference's DE cost for the same associations, bounds and previous motion.

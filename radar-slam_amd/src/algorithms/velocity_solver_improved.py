@@ -12,7 +12,9 @@ Device work (librsl):
   the wrapped, regularised cost (:223-266) with differential evolution (seed 42, :387-396 and :421-430).  That cost
   has one basin per 2 pi / k of radial velocity (0.0195 m/s at 77 GHz, dt = 0.1 s), so DE's answer is one local
   minimum among millions.  Step 1 runs projected Gauss-Newton in (v_x, v_y) from every point of a grid with half the
-  wrap period as spacing over the same box (every basin is entered), refines the best basins and the initial guess
+  wrap period as spacing over the same box (a heuristic: the sum of N ridge families has cells smaller than the wrap
+  period, so not every basin is guaranteed to be entered; what is checked is the cost <= DE contract below, and the
+  grid's cost is measured in tests/test_gpu_wrapped.py::test_wrapped_search_latency), refines the best basins and the initial guess
   in 3-D and keeps the lowest cost; step 2 refines in 6-D from step 1's answer, the initial guess and a 512 x 512
   start grid.  Parity contract: cost <= the reference's
   DE cost (tests/test_gpu_wrapped.py against tests/golden/golden_wrapped.npz).

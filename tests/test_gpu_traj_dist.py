@@ -4,7 +4,11 @@ group and run TrajectoryReducer.step for 4 steps + finalize, i.e. rsl/traj.py's 
 summary all-gather, rsl_traj_stitch / rsl_traj_apply, the pose gather to rank 0 and the rank-0 streaming smoothing.
 Rank 0's trajectory is checked against the oracle restatement of pose_integration.py:67-167 over the whole
 concatenated sequence (step, rank, frame): smoothed positions (integrate_positions(smoothing=True)) and rotations
-(integrate_rotations) to 1e-9."""
+(integrate_rotations) to 1e-9.
+
+VERDICT r3 next #7: the same at world size 1 over `nccl` (RCCL) in a fresh spawned process, so the device-tensor
+collective branches (`all_gather_into_tensor` of the summaries and `gather` of the poses on device tensors,
+rsl/traj.py step / _gather) execute as shipped on the one GPU a box has; the test asserts the reducer took them."""
 import os
 import socket
 
@@ -16,7 +20,7 @@ import radar_oracle as O
 pytestmark = pytest.mark.gpu
 
 DT = 0.1
-STEPS, F, WORLD, WINDOW = 4, 37, 2, 5
+STEPS, F, WINDOW = 4, 37, 5
 
 
 def _free_port():
@@ -27,13 +31,13 @@ def _free_port():
     return p
 
 
-def _inputs():
+def _inputs(world):
     rs = np.random.RandomState(21)
-    n = STEPS * WORLD * F
+    n = STEPS * world * F
     return rs.randn(n, 3), 0.3 * rs.randn(n, 3)
 
 
-def _worker(rank, port, out):
+def _worker(rank, port, out, backend, world):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, 'radar-slam_amd'))
@@ -43,12 +47,16 @@ def _worker(rank, port, out):
     from rsl.traj import TrajectoryReducer
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    if backend == 'nccl':
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     ctx = rsl.get_context(0)
-    vel, om = _inputs()
+    vel, om = _inputs(world)
     red = TrajectoryReducer(ctx, F, dt=DT, smoothing_window=WINDOW, keep=True)
+    assert red.on and red.gloo == (backend == 'gloo')  # nccl: the device-tensor collective branches
     for s in range(STEPS):
-        g0 = (s * WORLD + rank) * F
+        g0 = (s * world + rank) * F
         v = ctx.to_dev(np.ascontiguousarray(vel[g0:g0 + F]))
         w = ctx.to_dev(np.ascontiguousarray(om[g0:g0 + F]))
         red.step(v, vstride=3, nv=3, omega=w, ostride=3)
@@ -61,13 +69,15 @@ def _worker(rank, port, out):
     dist.destroy_process_group()
 
 
-def test_reducer_two_ranks_on_device(tmp_path):
+@pytest.mark.parametrize('backend,world', [('gloo', 2), ('nccl', 1)])
+def test_reducer_on_device(tmp_path, backend, world):
     import torch.multiprocessing as mp
     from scipy.spatial.transform import Rotation
     out = str(tmp_path / 'traj.npz')
-    mp.start_processes(_worker, args=(_free_port(), out), nprocs=WORLD, join=True, start_method='spawn')
+    mp.start_processes(_worker, args=(_free_port(), out, backend, world), nprocs=world, join=True,
+                       start_method='spawn')
     z = np.load(out)
-    vel, om = _inputs()
+    vel, om = _inputs(world)
     ts = np.arange(len(vel)) * DT
     ref_pos = O.integrate_positions(vel, ts, smoothing=True, window=WINDOW)
     ref_rot = O.integrate_rotations(om, ts)

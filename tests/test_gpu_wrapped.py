@@ -152,3 +152,30 @@ def test_wrapped_solvers_vs_reference_de_wide(ctx, golden, case):
         assert res['cost'] <= float(de.min()) * (1 + TOL), (res['cost'], float(de.min()))
         if bool(z['success']):  # bounds follow the reference's update after a converged run
             assert np.array_equal(np.array(opt.adaptive_bounds['velocity_bounds']), z['bounds_after'])
+
+
+@pytest.mark.parametrize('case', ['adv_n60', 'imp_n20'])
+def test_wrapped_search_latency(ctx, golden, case, record_property):
+    """the stage-1 grid of rsl_wrapped_search at the reference's own scale (+-50 m/s box, 77 GHz, dt 0.1:
+    spacing 0.5 x 2 pi / k = 9.7 mm/s, ~10^4 points per axis, ~10^8 starts) — its per-call latency is measured and
+    printed (DESIGN.md §3 records it), and bounded here so a regression in the start count cannot go unnoticed."""
+    import math
+    import time
+    import torch
+    from rsl import ops
+    z = golden(f'wrapped_{case}')
+    k = 4 * np.pi * 0.1 / float(z['lambda_c'])
+    pos, ang, y = _geometry(z)
+    lo = [-50.0, -50.0, -10.0, -10.0, -10.0, -10.0]
+    hi = [50.0, 50.0, 10.0, 10.0, 10.0, 10.0]
+    ops.wrapped_search(pos, ang, y, k, mode=0, lo=lo, hi=hi, nv=3, ctx=ctx)  # warm-up (code objects, scratch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    x, cost = ops.wrapped_search(pos, ang, y, k, mode=0, lo=lo, hi=hi, nv=3, ctx=ctx)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    g = min(32768, math.ceil(100.0 / (0.5 * 2 * math.pi / k)))
+    print(f'wrapped_search {case}: n={len(y)} targets, grid {g} x {g} = {g * g:.3g} starts, '
+          f'{dt * 1e3:.1f} ms per call, cost {cost:.4f}')
+    record_property('wrapped_search_ms', dt * 1e3)
+    assert np.isfinite(cost) and dt < 5.0
