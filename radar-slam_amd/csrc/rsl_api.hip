@@ -377,8 +377,8 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   if (base_method != RSL_METHOD_MUSIC && base_method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
   const bool music = base_method == RSL_METHOD_MUSIC;
-  if (toep && music && !steer_c128)
-    return fail(h, RSL_ERR_INVALID, "rsl_doa: the Toeplitz MUSIC path needs the fp64 steering table");
+  if (toep && !steer_c128)
+    return fail(h, RSL_ERR_INVALID, "rsl_doa: the Toeplitz path needs the fp64 steering table (exact re-scan)");
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
   Scope sc(h, RSL_K_DOA_SCAN);
@@ -417,7 +417,7 @@ int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const voi
   if (method != RSL_METHOD_MUSIC && method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: unknown method");
   const bool music = method == RSL_METHOD_MUSIC;
-  if (music && !steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: MUSIC needs the fp64 steering table");
+  if (!steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: needs the fp64 steering table (exact re-scan)");
   if (!rsl::toep_table_fits(G, A))
     return fail(h, RSL_ERR_UNSUPPORTED, "rsl_doa_extras: grid too large for the Toeplitz path (use rsl_doa)");
   if (!ncell_dev && ncell <= 0) return RSL_OK;

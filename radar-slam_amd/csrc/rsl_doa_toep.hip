@@ -241,37 +241,68 @@ RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
   for (int k = 0; k < NCOPY; ++k) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,1]" : "=v"(dst[k]) : "v"(s[k]));
 }
 
-// Exact fp64 scan of one cell (MUSIC near-degenerate path): key = P if M - P > 1e-12 else -1, first index.
-template <int MA>
-RSL_DEV void exact_scan(const float2 (&s)[MA], int A, int G, const double* __restrict__ steer64, int& idx,
-                        float& gval) {
-  double sr[MA], si[MA], pw = 0.0;
+// Ambiguity bound of the f16 hi/lo scan, relative to a cell's maximum: a cell whose best grid value is not at least
+// this far above every other grid value (its top-2 gap) is re-scanned exactly in fp64 (coop_scan), so that the grid
+// index is the fp64 argmax of the cell's own fp32 signature (no scan-caused flips).  The scan's
+// error is far smaller: the dropped T_lo r_lo term is <= 2^-22 sum |T_k| |r_k| and the fp32 autocorrelation and MFMA
+// accumulation add a few fp32 ulps of that sum (measured against the fp64 scan of the same signatures:
+// tests/test_gpu_spectrum.py::test_toeplitz_spectrum_matches_f32_scan, max 3.8e-6 of M on den = M - P; the flips the
+// round-3 build made had gaps <= 8.6e-8).  ~0.2 % of cfg2 cells fall inside the bound.
+constexpr float kAmbRel = 2e-6f;
+
+// Exact fp64 scan of ONE cell by the whole wave (lanes split the grid points; wave-uniform cell c): the key is P if
+// M - P > 1e-12 (MUSIC, angle_estimation.py:149-152) else -1, P for beamforming; first index of the maximum key, as
+// np.argmax.  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table.  Returns (index, P at it) on every lane.
+template <int MA, bool MUSIC>
+__device__ __attribute__((noinline)) void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
+                       long long c, int A, size_t plane, size_t fstride, int G, const double* __restrict__ steer64,
+                       int& idx, float& gval) {
+  // the cell's signature in scalar registers (wave-uniform): the rare path adds no vector-register pressure to the
+  // kernel's hot loop (whose 128-VGPR budget sets 4 waves per SIMD)
+  const int fx = __builtin_amdgcn_readfirstlane(cfr[c]), fy = __builtin_amdgcn_readfirstlane(crc[c]);
+  const float2* base = rds + (size_t)fx * fstride + fy;
+  float sr[MA], si[MA];
+  double pw = 0.0;
 #pragma unroll
   for (int m = 0; m < MA; ++m) {
-    sr[m] = s[m].x;
-    si[m] = s[m].y;
-    pw += sr[m] * sr[m] + si[m] * si[m];
+    const float2 z = m < A ? base[(size_t)m * plane] : make_float2(0.f, 0.f);
+    sr[m] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z.x)));
+    si[m] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z.y)));
+    pw += (double)sr[m] * sr[m] + (double)si[m] * si[m];
   }
   const double sc = pw > 0.0 ? 1.0 / sqrt(pw) : 1.0;
+  const int lane = threadIdx.x & 63;
   double best = -INFINITY, bp = 0.0;
-  int bi = 0;
-  for (int g = 0; g < G; ++g) {
+  int bi = G;
+#pragma unroll 1
+  for (int g = lane; g < G; g += 64) {  // ascending g per lane: strict '>' keeps the first index
     const double* a = steer64 + (size_t)g * A * 2;
     double zr = 0.0, zi = 0.0;
-#pragma unroll
-    for (int m = 0; m < MA; ++m) {
-      if (m < A) {
-        const double ar = a[2 * m], ai = a[2 * m + 1];
-        zr += ar * sr[m] + ai * si[m];
-        zi += ar * si[m] - ai * sr[m];
-      }
+#pragma unroll 2
+    for (int m = 0; m < A && m < MA; ++m) {
+      const double ar = a[2 * m], ai = a[2 * m + 1];
+      const double xr = sr[m], xi = si[m];
+      zr += ar * xr + ai * xi;
+      zi += ar * xi - ai * xr;
     }
     const double p = (zr * zr + zi * zi) * sc * sc;
-    const double key = ((double)A - p > 1e-12) ? p : -1.0;
+    const double key = MUSIC ? (((double)A - p > 1e-12) ? p : -1.0) : p;
     if (key > best) {
       best = key;
       bi = g;
       bp = p;
+    }
+  }
+  // wave argmax of (key, index): larger key, then lower index
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ok = __shfl_xor(best, off);
+    const int oi = __shfl_xor(bi, off);
+    const double op = __shfl_xor(bp, off);
+    if (ok > best || (ok == best && oi < bi)) {
+      best = ok;
+      bi = oi;
+      bp = op;
     }
   }
   idx = bi;
@@ -336,16 +367,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   // The argmax (and gmax) of a pass is stored at the start of the NEXT pass, after the wait for that pass's prefetched
   // signatures: stored at the end of its own pass it sat in front of that wait (stores count in vmcnt, and a store
   // under a branch makes the compiler wait for vmcnt(0)), so every pass waited out a store round trip.
-  int pc = -1;  // pending store: cell (-1: none; cell counts < 2^31, checked by the launcher), grid index, gmax
+  // pending store of the previous pass (wave-uniform flag; its cell is (ch - stride) 64 + lane, recomputed rather
+  // than kept in a register across the tile loop)
+  bool pend = false;
   int pidx = 0;
   float pgv = 0.f;
   for (; ch < nch; ch += stride) {
     float2 s[MA];
 #pragma unroll
     for (int m = 0; m < MA; ++m) s[m] = ns[m];
-    if (pc >= 0) {
-      out_idx[pc] = pidx;
-      if constexpr (GMAX) out_gmax[pc] = pgv;
+    if (pend) {
+      const long long cp = (ch - stride) * 64 + lane;
+      if (cp < ncell) {
+        out_idx[cp] = pidx;
+        if constexpr (GMAX) out_gmax[cp] = pgv;
+      }
     }
     const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
@@ -429,7 +465,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     // in-tile values ascend in row ((i&3) + 8(i>>2) + 4h): the first index wins as in np.argmax.  Rows past G
     // replicate row G-1 and so never win.
     float best0 = -INFINITY, best1 = -INFINITY;
-    int bt0 = 0, bt1 = 0;
+    float second0 = __int_as_float(INT_MIN), second1 = __int_as_float(INT_MIN);  // below every value as ints
+    int bt01 = 0;  // record tile of column tile 0 (bits 0-15) and 1 (bits 16-31): one register
+    auto set_bt = [&](int sh, int t) { bt01 = (bt01 & ~(0xFFFF << sh)) | (t << sh); };
     double sv0[8], sv1[8];  // record tiles as 64-bit register pairs (copied with v_pk_mov_b32)
 #pragma unroll
     for (int k = 0; k < 8; ++k) sv0[k] = sv1[k] = 0.0;
@@ -474,17 +512,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         }
         return;
       }
+      // second*: the largest tile maximum of the other tiles (ambiguity test at the end of the pass)
       if (m0 > best0) {
+        second0 = best0;
         best0 = m0;
-        bt0 = t;
+        set_bt(0, t);
         if constexpr (DBG == 7) copy_tile<1>(sv0, acc0);
         else if constexpr (DBG != 1) copy_tile(sv0, acc0);
+      } else {
+        second0 = fmaxf(second0, m0);
       }
       if (m1 > best1) {
+        second1 = best1;
         best1 = m1;
-        bt1 = t;
+        set_bt(16, t);
         if constexpr (DBG == 7) copy_tile<1>(sv1, acc1);
         else if constexpr (DBG != 1) copy_tile(sv1, acc1);
+      } else {
+        second1 = fmaxf(second1, m1);
       }
     };
     // SPEC: the whole spectrum of both column tiles, cell-blocked f32 [ceil(n / 32)][G][32] (RSL_DOA_SPEC_BLOCKED):
@@ -551,7 +596,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc, 0, 0, 0);
       };
-      auto rec = [&](int t, const floatx16& acc, float& best, int& bt, double (&sv)[8]) {
+      auto rec = [&](int t, const floatx16& acc, float& best, float& second, int sh, double (&sv)[8]) {
         if constexpr (DBG == 8) {  // no epilogue: one max per tile keeps the accumulator live
           best = fmaxf(best, acc[t & 15]);
           return;
@@ -564,73 +609,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
           for (int k = 0; k < 8; ++k) sv[k] = d[k];
           return;
         }
-        // the running best joins the max tree (same 8 v_max3): mb = max(best, tile) updates best without a move in
-        // the record branch; mb > best <=> the tile max > best (the tile max as ints is mb whenever it wins)
-        const float mb = tile_max(acc, best);
-        const bool r = mb > best;
-        best = mb;
+        // the running SECOND joins the max tree (same 8 v_max3): m2 = max(second, tile max); since second <= best,
+        // m2 > best <=> the tile max > best.  A record moves best to second; otherwise second = m2 (the largest tile
+        // maximum of the other tiles: the end-of-pass ambiguity test)
+        const float m2 = tile_max(acc, second);
+        const bool r = m2 > best;
+        second = r ? best : m2;
         if (r) {
-          bt = t;
+          best = m2;
+          set_bt(sh, t);
           if constexpr (DBG != 1) copy_tile(sv, acc);
-        }
-      };
-      // record commit after the tile max m of a column tile's accumulator (first tile: unconditional)
-      auto commit = [&](int t, float m, const floatx16& acc, float& best, int& bt, double (&sv)[8]) {
-        if (t == 0) {
-          typedef double doublex8 __attribute__((ext_vector_type(8)));
-          const doublex8 d = __builtin_bit_cast(doublex8, acc);
-          best = m;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) sv[k] = d[k];
-          return;
-        }
-        if (m > best) {
-          best = m;
-          bt = t;
-          copy_tile(sv, acc);
         }
       };
       if constexpr (DBG == 9) {  // no tile loop (prologue, loads and the index resolution only)
         best0 = __builtin_bit_cast(float, b0h[0].x ^ b1l[0].y);
         best1 = __builtin_bit_cast(float, b1h[0].z ^ b0l[0].w);
-      } else if constexpr (DBG == 12) {
-        // Interleaved skew: each column tile's tile-max VALU is issued BETWEEN the other column tile's three MFMAs
-        // (one MFMA, three VALU, ...) instead of as a block after them, so that the matrix pipe keeps running while
-        // the wave does its epilogue; the record copies (a branch) follow each group.  Pipeline per tile t:
-        //   [chain1(t) | max(acc0(t))] -> copy0(t) -> [max(acc1(t)) | chain0(t + 1)] -> copy1(t)
-        // Same products, same record order as the block schedule.
-        lda(0);
-        chain(acc0, x0h, x0l);
-#pragma unroll
-        for (int t = 0; t < NTC; ++t) {
-          __builtin_amdgcn_sched_barrier(0);
-          chain(acc1, x1h, x1l);
-          const float m0 = tile_max(acc0);
-          const bool r0 = t == 0 || m0 > best0;
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 < NTC) lda(t + 1);
-          if (r0) commit(t, m0, acc0, best0, bt0, sv0);
-          __builtin_amdgcn_sched_barrier(0);
-          const float m1 = tile_max(acc1);
-          const bool r1 = t == 0 || m1 > best1;
-          if (t + 1 < NTC) {
-            chain(acc0, x0h, x0l);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (r1) commit(t, m1, acc1, best1, bt1, sv1);
-        }
       } else {
       lda(0);
       chain(acc0, x0h, x0l);
@@ -639,12 +632,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       for (int t = 0; t < NTC; ++t) {
         if (t + 1 < NTC) lda(t + 1);
         __builtin_amdgcn_sched_barrier(0);
-        rec(t, acc0, best0, bt0, sv0);
+        rec(t, acc0, best0, second0, 0, sv0);
         spec_tile(t, acc0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NTC) chain(acc0, x0h, x0l);
         __builtin_amdgcn_sched_barrier(0);
-        rec(t, acc1, best1, bt1, sv1);
+        rec(t, acc1, best1, second1, 16, sv1);
         spec_tile(t, acc1, 1);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < NTC) chain(acc1, x1h, x1l);
@@ -661,46 +654,73 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         spec_tile(t, acc1, 1);
       }
     }
-    int i0 = 15, i1 = 15;
+    // Index resolution and ambiguity, per column tile: theta = best (1 - kAmbRel); i = the first of the record tile's
+    // 16 values >= theta, n = how many there are.  n == 1: that value is the lane's maximum and every other value of
+    // the lane is below theta, so i is its exact argmax; n >= 2, a tile maximum of another tile >= theta, or a
+    // non-positive best (a zero signature): ambiguous, re-scanned in fp64 below.
+    int i0 = 15, i1 = 15, n0 = 0, n1 = 0;
     {
       const floatx16 r0 = __builtin_bit_cast(floatx16, sv0), r1 = __builtin_bit_cast(floatx16, sv1);
+      const float th0 = best0 * (1.f - kAmbRel), th1 = best1 * (1.f - kAmbRel);
 #pragma unroll
-      for (int i = 14; i >= 0; --i) {
-        i0 = (r0[i] == best0) ? i : i0;
-        i1 = (r1[i] == best1) ? i : i1;
+      for (int i = 15; i >= 0; --i) {
+        const bool g0 = r0[i] >= th0, g1 = r1[i] >= th1;
+        i0 = g0 ? i : i0;
+        i1 = g1 ? i : i1;
+        n0 += g0;
+        n1 += g1;
       }
     }
-    int g0 = 32 * bt0 + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
-    int g1 = 32 * bt1 + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
-    // merge the two K-half lanes of each column (first index wins on ties)
+    bool amb0 = n0 != 1 || second0 >= best0 * (1.f - kAmbRel) || !(best0 > 0.f);
+    bool amb1 = n1 != 1 || second1 >= best1 * (1.f - kAmbRel) || !(best1 > 0.f);
+    int g0 = 32 * (bt01 & 0xFFFF) + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
+    int g1 = 32 * (bt01 >> 16) + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
+    // merge the two K-half lanes of each column (first index wins on ties); ambiguous if the winner is, or if the
+    // loser's maximum is within the bound of the winner's (an exact tie included)
     {
       const float ob0 = __shfl_xor(best0, 32), ob1 = __shfl_xor(best1, 32);
       const int og0 = __shfl_xor(g0, 32), og1 = __shfl_xor(g1, 32);
+      const bool oa0 = __shfl_xor((int)amb0, 32) != 0, oa1 = __shfl_xor((int)amb1, 32) != 0;
       const bool tk0 = (ob0 > best0) | ((ob0 == best0) & (og0 < g0));
       const bool tk1 = (ob1 > best1) | ((ob1 == best1) & (og1 < g1));
+      const float lo0 = tk0 ? best0 : ob0, lo1 = tk1 ? best1 : ob1;
       best0 = tk0 ? ob0 : best0;
       g0 = tk0 ? og0 : g0;
+      amb0 = (tk0 ? oa0 : amb0) || lo0 >= best0 * (1.f - kAmbRel);
       best1 = tk1 ? ob1 : best1;
       g1 = tk1 ? og1 : g1;
+      amb1 = (tk1 ? oa1 : amb1) || lo1 >= best1 * (1.f - kAmbRel);
     }
     float best = h ? best1 : best0;  // own cell = column tile h
     int bidx = h ? g1 : g0;
+    bool amb = h ? amb1 : amb0;
     if (bidx >= G) bidx = G - 1;
     float gval = best * (1.0f / kToepScale);
-    if constexpr (MUSIC) {
-      if (best >= mthr && c < ncell) {  // rare: reload the signature (keeps s dead across the tile loop)
-        float2 sr[MA];
-        load_sig_c<MA>(rds, cfr, crc, c, true, A, plane, fstride, sr);
-        exact_scan<MA>(sr, A, G, steer64, bidx, gval);
+    // MUSIC: the reference's den > 1e-12 rule can only matter when the maximum is within rounding of M
+    if constexpr (MUSIC) amb = amb || best >= mthr;
+    // exact fp64 re-scan of the ambiguous cells, one cell at a time by the whole wave (no lane divergence)
+    unsigned long long fl = __ballot(amb && c < ncell);
+    while (fl) {
+      const int src = __builtin_ctzll(fl);
+      fl &= fl - 1;
+      int xi;
+      float xg;
+      coop_scan<MA, MUSIC>(rds, cfr, crc, ch * 64 + src, A, plane, fstride, G, steer64, xi, xg);
+      if (lane == src) {
+        bidx = xi;
+        gval = xg;
       }
     }
-    pc = c < ncell ? (int)c : -1;
+    pend = true;
     pidx = bidx;
     pgv = gval;
   }
-  if (pc >= 0) {
-    out_idx[pc] = pidx;
-    if constexpr (GMAX) out_gmax[pc] = pgv;
+  if (pend) {
+    const long long cp = (ch - stride) * 64 + lane;
+    if (cp < ncell) {
+      out_idx[cp] = pidx;
+      if constexpr (GMAX) out_gmax[cp] = pgv;
+    }
   }
 }
 
@@ -727,7 +747,6 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 9) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 9, 12, true>;  // no tile loop
         if (v == 10) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 10, 12, true>;  // L2-resident signatures
         if (v == 11) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 11, 12, true>;  // prefetch 2 passes ahead
-        if (v == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 12, 12, true>;  // interleaved skew
       }
     }
   }
@@ -759,7 +778,7 @@ hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int 
                            int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
                            double esprit_scale, double* out_esprit, double* out_phase, float* out_spec) {
   if (A < 1 || A > 16 || (ntiles32 & 1) || ncell_host >= (1LL << 31) - 64) return hipErrorInvalidValue;
-  if (music && !steer64) return hipErrorInvalidValue;
+  if (!steer64) return hipErrorInvalidValue;  // the exact fp64 re-scan of ambiguous cells
   if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
   const long long max_blocks = ncell_dev ? 0 : (ncell_host + 255) / 256;  // 4 waves x 64 cells
   if (!ncell_dev && ncell_host <= 0) return hipSuccess;

@@ -7,7 +7,8 @@
 //
 // The sequential recurrences are associative, so each is a block-wide inclusive scan: positions are the prefix
 // sum of the per-step increments, orientations the ordered prefix product of the per-step rotation quaternions
-// (q_i = q_{i-1} (x) exp(omega_{i-1} dt / 2)).  One 1024-thread workgroup scans one frame block: each thread
+// (q_i = q_{i-1} (x) exp(omega_{i-1} dt / 2)).  One wave (k_traj_scan_wave, blocks up to 65536 frames) or one
+// 1024-thread workgroup (k_traj_scan, longer blocks) scans one frame block: each thread
 // reduces a contiguous chunk serially, the chunk totals are scanned in LDS, then each chunk is rewritten with
 // its exclusive prefix.  Frames sharded over GPUs are stitched by rsl/traj.py from 16-double block summaries.
 #include "rsl_common.h"
@@ -118,6 +119,75 @@ __global__ __launch_bounds__(kTrajThreads) void k_traj_scan(const double* __rest
   }
 }
 
+// The same scan by ONE wave (64 lanes, no LDS, no barrier), for blocks of up to kTrajWaveMax frames (the bench's
+// 2000-frame batches): lane t reduces its contiguous chunk serially, the 64 chunk totals are scanned across lanes by
+// __shfl_up (Hillis-Steele; quaternion products keep left-to-right order), then each chunk is rewritten from its
+// exclusive prefix.  A 64-thread launch needs one free wave slot anywhere on the chip, so on a third stream it starts
+// at once beside the other batch's kernels; the 1024-thread form waited for a whole CU to drain (k_traj_scan: 24 us
+// to 5.7 ms in the r3f trace, 2.8 ms average).
+constexpr long kTrajWaveMax = 1L << 16;
+__global__ __launch_bounds__(64) void k_traj_scan_wave(const double* __restrict__ vel, int vstride, int nv,
+                                                       const double* __restrict__ om, int ostride,
+                                                       const double* __restrict__ ts, double dt, long F, int method,
+                                                       double* __restrict__ pos, double* __restrict__ quat,
+                                                       double* __restrict__ summary) {
+  const int t = threadIdx.x;
+  const long per = (F + 63) / 64;
+  const long b = t * per, e = min(F, b + per);
+  auto V = [&](long i, int a) -> double { return a < nv ? vel[i * vstride + a] : 0.0; };
+  auto W = [&](long i, int a) -> double { return om ? om[i * ostride + a] : 0.0; };
+  auto DT = [&](long i) -> double { return ts ? ts[i + 1] - ts[i] : dt; };  // np.diff(timestamps)[i]
+  double p[3] = {0.0, 0.0, 0.0};
+  Quat q{1.0, 0.0, 0.0, 0.0};
+  for (long i = max(b, 1L); i < e; ++i) {
+    const double d = DT(i - 1);
+    for (int a = 0; a < 3; ++a) p[a] += method == 0 ? 0.5 * d * (V(i - 1, a) + V(i, a)) : d * V(i - 1, a);
+    q = qmul(q, rotvec_quat(W(i - 1, 0), W(i - 1, 1), W(i - 1, 2), d));
+  }
+  // inclusive scan of the chunk totals across the wave
+  for (int off = 1; off < 64; off <<= 1) {
+    double pp[3];
+    for (int a = 0; a < 3; ++a) pp[a] = __shfl_up(p[a], off);
+    const Quat qq{__shfl_up(q.w, off), __shfl_up(q.x, off), __shfl_up(q.y, off), __shfl_up(q.z, off)};
+    if (t >= off) {
+      for (int a = 0; a < 3; ++a) p[a] += pp[a];
+      q = qmul(qq, q);
+    }
+  }
+  // exclusive prefix = the inclusive value of lane t - 1
+  double ep[3];
+  for (int a = 0; a < 3; ++a) ep[a] = __shfl_up(p[a], 1);
+  Quat eq{__shfl_up(q.w, 1), __shfl_up(q.x, 1), __shfl_up(q.y, 1), __shfl_up(q.z, 1)};
+  if (t == 0) {
+    ep[0] = ep[1] = ep[2] = 0.0;
+    eq = Quat{1.0, 0.0, 0.0, 0.0};
+  }
+  for (long i = b; i < e; ++i) {
+    if (i >= 1) {
+      const double d = DT(i - 1);
+      for (int a = 0; a < 3; ++a) ep[a] += method == 0 ? 0.5 * d * (V(i - 1, a) + V(i, a)) : d * V(i - 1, a);
+      eq = qmul(eq, rotvec_quat(W(i - 1, 0), W(i - 1, 1), W(i - 1, 2), d));
+    }
+    for (int a = 0; a < 3; ++a) pos[i * 3 + a] = ep[a];
+    quat[i * 4 + 0] = eq.w;
+    quat[i * 4 + 1] = eq.x;
+    quat[i * 4 + 2] = eq.y;
+    quat[i * 4 + 3] = eq.z;
+  }
+  if (t == 63 && summary) {
+    for (int a = 0; a < 3; ++a) summary[a] = p[a];
+    summary[3] = q.w;
+    summary[4] = q.x;
+    summary[5] = q.y;
+    summary[6] = q.z;
+    for (int a = 0; a < 3; ++a) {
+      summary[7 + a] = V(F - 1, a);
+      summary[10 + a] = V(0, a);
+      summary[13 + a] = W(F - 1, a);
+    }
+  }
+}
+
 // pos[i] += base_p ; quat[i] = base_q (x) quat[i]   (base [7] device: p (3), q (4))
 __global__ __launch_bounds__(256) void k_traj_apply(double* __restrict__ pos, double* __restrict__ quat, long F,
                                                     const double* __restrict__ base) {
@@ -205,6 +275,11 @@ hipError_t launch_traj_scan(hipStream_t st, const double* vel, int vstride, int 
                             const double* ts, double dt, long F, int method, double* pos, double* quat,
                             double* summary) {
   if (F <= 0) return hipSuccess;
+  if (F <= kTrajWaveMax) {
+    hipLaunchKernelGGL(k_traj_scan_wave, dim3(1), dim3(64), 0, st, vel, vstride, nv, om, ostride, ts, dt, F, method,
+                       pos, quat, summary);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_traj_scan, dim3(1), dim3(kTrajThreads), 0, st, vel, vstride, nv, om, ostride, ts, dt, F,
                      method, pos, quat, summary);
   return hipGetLastError();

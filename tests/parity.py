@@ -8,6 +8,9 @@ reference's own fp64 values, or report it as unexplained.  Tolerances are stated
             the reference maximum, (g_ref_max - g_ref[gpu_idx]) / g_ref_max < 1e-6 (an fp32 near-tie,
             or the +-90 deg alias, whose gap is 0); the number of such flips is asserted against
             DOA_FLIP_FRAC * N_cells (each flip is a 0.5 deg miss, so it is counted, not just explained)
+  Of those flips none may be scan-caused (scan_flips): the GPU index must be the fp64 argmax of the
+            GPU's own fp32 signature, up to fp64-level ties (relative gap <= OWN_TIE_RGAP, e.g. the +-90 deg alias);
+            the remaining flips are RDS-caused (the fp32 RDS itself moves the argmax)
 * ESPRIT:   |deg_gpu - deg_ref| <= ESPRIT_TOL_DEG (= 1e-3 rad, the north-star DoA tolerance)
 * velocity: cost within VEL_COST_RTOL relative; (v_x, v_y) within VEL_ATOL m/s when well conditioned
 """
@@ -19,6 +22,7 @@ RDS_ATOL_REL = 1e-5
 PEAK_RTOL = 2e-5
 DOA_RGAP = 1e-6
 DOA_FLIP_FRAC = 2e-4
+OWN_TIE_RGAP = 1e-12
 ESPRIT_TOL_DEG = float(np.degrees(1e-3))
 VEL_COST_RTOL = 1e-6
 VEL_ATOL = 1e-4
@@ -93,3 +97,32 @@ def esprit_diff(gpu_deg, ref_deg):
     d = np.abs(gpu_deg - ref_deg)
     d[both_nan] = 0
     return float(np.nanmax(d) if d.size else 0.0), int((np.isnan(gpu_deg) != np.isnan(ref_deg)).sum())
+
+
+def scan_flips(gpu_idx, gpu_sigs, steer, method='music'):
+    """Scan-caused flips: cells whose GPU grid index is not the fp64 argmax of the GPU's OWN signature (gpu_sigs: the
+    fp32 RDS values of each cell, any scale), beyond fp64-level ties (gap <= OWN_TIE_RGAP relative).  Returns
+    (count, largest relative gap among them)."""
+    if len(gpu_idx) == 0:
+        return 0, 0.0
+    gs = np.asarray(gpu_sigs, np.complex128)
+    nrm = np.linalg.norm(gs, axis=1, keepdims=True)
+    gs = gs / np.where(nrm > 0, nrm, 1.0)
+    g = np.abs(gs @ steer.conj().T) ** 2
+    own = np.argmax(O.music_spectrum_closed(gs, steer), axis=1) if method == 'music' else np.argmax(g, axis=1)
+    n = np.arange(len(gpu_idx))
+    go = g[n, own]
+    rgap = (go - g[n, gpu_idx]) / np.where(go > 0, go, 1.0)
+    bad = (gpu_idx != own) & (rgap > OWN_TIE_RGAP)
+    return int(bad.sum()), float(rgap[bad].max()) if bad.any() else 0.0
+
+
+def spectrum_argmax_consistent(spec, idx, method='music', atol=2e-5):
+    """The grid index is a maximum of the written f32 spectrum up to the scan's precision: exactly the f16 scan's
+    argmax where its top-2 gap is clear, the fp64 argmax of the cell's signature where it was re-scanned (a near-tie
+    inside the scan's 2e-6 bound), so the written value there is within the den / power tolerance of the row max."""
+    n = np.arange(len(idx))
+    if method == 'music':
+        d = np.where(spec > 0, 1.0 / np.where(spec > 0, spec, 1.0), np.inf)
+        return bool(((d[n, idx] - d.min(axis=1)) <= atol).all())
+    return bool(((spec.max(axis=1) - spec[n, idx]) <= atol).all())

@@ -110,12 +110,11 @@ def test_doa_esprit_parity(runs, name):
         ii, jj = rc // cfg.num_chirps, rc % cfg.num_chirps
         sigs = np.stack([O.spatial_signature(ref, i, j) for i, j in zip(ii, jj)]) if len(rc) else np.zeros((0, A))
         nm, nu, ref_idx = P.doa_diff(r['gidx'][sl], sigs, steer, 'music', stats=stats)
-        flip = np.nonzero(r['gidx'][sl] != ref_idx)[0]
-        if len(flip):  # fp64 scan of the GPU's own fp32 RDS signature at each flip
-            gs = r['rds'][f][:, ii[flip], jj[flip]].T.astype(np.complex128)
-            gs = gs / np.linalg.norm(gs, axis=1, keepdims=True)
-            own = np.argmax(O.music_spectrum_closed(gs, steer), axis=1)
-            n_scan += int((own == ref_idx[flip]).sum())  # the GPU's RDS gives the oracle's answer: the scan flipped
+        # every sampled cell against the fp64 scan of the GPU's own fp32 RDS signature: none may differ (the device
+        # re-scans its near-ties in fp64), so each flip against the oracle is RDS-caused
+        ns, sgap = P.scan_flips(r['gidx'][sl], r['rds'][f][:, ii, jj].T, steer, 'music')
+        n_scan += ns
+        stats['scan_gap'] = max(stats.get('scan_gap', 0.0), sgap)
         tot_m += nm
         tot_u += nu
         tot_n += len(sl)
@@ -125,9 +124,10 @@ def test_doa_esprit_parity(runs, name):
         ph = O.observed_phase(sigs)
         dph = np.angle(np.exp(1j * (r['phase'][sl] - ph)))
         assert np.abs(dph).max() < 1e-4
-    print(f'\n{name}: DoA flips {tot_m} of {tot_n} cells (alias {stats.get("alias", 0)}; scan-caused {n_scan}: an '
-          f'fp64 scan of the GPU\'s own RDS gives the oracle\'s index; RDS-caused {tot_m - n_scan}), largest reference '
-          f'relative gap of a flip {stats.get("max_rgap", 0.0):.2e}')
+    print(f'\n{name}: DoA flips {tot_m} of {tot_n} cells against the oracle (alias {stats.get("alias", 0)}; all '
+          f'RDS-caused), largest reference relative gap of a flip {stats.get("max_rgap", 0.0):.2e}; scan-caused '
+          f'(GPU index != fp64 argmax of its own signature): {n_scan}')
+    assert n_scan == 0, (name, n_scan, stats)
     assert tot_u == 0, (name, tot_m, tot_u, stats)
     assert tot_m <= P.doa_flip_budget(tot_n, A), (name, tot_m, tot_n, stats)
 

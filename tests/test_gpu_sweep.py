@@ -88,12 +88,14 @@ def test_random_scene_parity(ctx, k):
         sigs = np.stack([O.spatial_signature(ref, i_, j_) for i_, j_ in zip(ii, jj)])
         nm, nun, _ = P.doa_diff(r['gidx'][cs], sigs, steer, cfg.method, stats=stats)
         assert nun == 0, (k, f, nm, nun, stats)
+        ns, sgap = P.scan_flips(r['gidx'][cs], rds[f][:, ii, jj].T, steer, cfg.method)
+        assert ns == 0, (k, f, 'scan-caused flips', ns, sgap)
         tot_m += nm
         tot_n += len(rc)
         if spectrum:  # den = 1/spectrum against the oracle's fp64 M - |a^H s|^2 (MUSIC), P itself (beamforming)
             got = spec[cs]
             n = np.arange(len(rc))
-            assert (got[n, r['gidx'][cs]] == got.max(axis=1)).all(), k
+            assert P.spectrum_argmax_consistent(got.astype(np.float64), r['gidx'][cs], cfg.method), k
             if cfg.method == 'music':
                 want = O.music_spectrum_closed(sigs, steer)
                 assert ((got > 0) == (want > 0)).all(), k
