@@ -254,7 +254,7 @@ constexpr float kAmbRel = 2e-6f;
 // M - P > 1e-12 (MUSIC, angle_estimation.py:149-152) else -1, P for beamforming; first index of the maximum key, as
 // np.argmax.  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table.  Returns (index, P at it) on every lane.
 template <int MA, bool MUSIC>
-__device__ __attribute__((noinline)) void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
+RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
                        long long c, int A, size_t plane, size_t fstride, int G, const double* __restrict__ steer64,
                        int& idx, float& gval) {
   // the cell's signature in scalar registers (wave-uniform): the rare path adds no vector-register pressure to the
@@ -369,19 +369,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   // under a branch makes the compiler wait for vmcnt(0)), so every pass waited out a store round trip.
   // pending store of the previous pass (wave-uniform flag; its cell is (ch - stride) 64 + lane, recomputed rather
   // than kept in a register across the tile loop)
-  bool pend = false;
+  int pc = -1;  // pending store: cell (-1: none; cell counts < 2^31, checked by the launcher), grid index, gmax
   int pidx = 0;
   float pgv = 0.f;
   for (; ch < nch; ch += stride) {
     float2 s[MA];
 #pragma unroll
     for (int m = 0; m < MA; ++m) s[m] = ns[m];
-    if (pend) {
-      const long long cp = (ch - stride) * 64 + lane;
-      if (cp < ncell) {
-        out_idx[cp] = pidx;
-        if constexpr (GMAX) out_gmax[cp] = pgv;
-      }
+    if (pc >= 0) {
+      out_idx[pc] = pidx;
+      if constexpr (GMAX) out_gmax[pc] = pgv;
     }
     const long long c = ch * 64 + lane;  // this lane's own cell
     const long long nx = ch + stride;
@@ -698,8 +695,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     float gval = best * (1.0f / kToepScale);
     // MUSIC: the reference's den > 1e-12 rule can only matter when the maximum is within rounding of M
     if constexpr (MUSIC) amb = amb || best >= mthr;
-    // exact fp64 re-scan of the ambiguous cells, one cell at a time by the whole wave (no lane divergence)
-    unsigned long long fl = __ballot(amb && c < ncell);
+    // ambiguous: marked -1 - index for k_doa_fixup (the exact fp64 re-scan, launched right after this kernel; kept
+    // out of this kernel so that its register allocation stays that of the scan loop)
+    if (amb) bidx = -1 - bidx;
+    pc = c < ncell ? (int)c : -1;
+    pidx = bidx;
+    pgv = gval;
+  }
+  if (pc >= 0) {
+    out_idx[pc] = pidx;
+    if constexpr (GMAX) out_gmax[pc] = pgv;
+  }
+}
+
+// Exact fp64 argmax of the cells k_doa_toep marked ambiguous (out_idx < 0: its f16 top-2 gap was inside kAmbRel, or a
+// MUSIC maximum within rounding of M): each wave reads 64 consecutive indices, and every marked cell is re-scanned by
+// the whole wave (coop_scan: lanes split the grid points).  Grid-stride over the cells; ~0.2 % of cfg2 cells.
+template <int MA, bool MUSIC>
+__global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
+                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
+                                                   const long long* __restrict__ ncell_dev, long long ncell_host, int G,
+                                                   const double* __restrict__ steer64, int* __restrict__ out_idx,
+                                                   float* __restrict__ out_gmax) {
+  const long long ncell = list_count(ncell_dev, ncell_host);
+  const int lane = threadIdx.x & 63;
+  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
+  const long long nch = (ncell + 63) >> 6;
+  for (long long ch = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); ch < nch; ch += (long long)gridDim.x * 4) {
+    const long long c = ch * 64 + lane;
+    const int v = c < ncell ? out_idx[c] : 0;
+    unsigned long long fl = __ballot(v < 0);
     while (fl) {
       const int src = __builtin_ctzll(fl);
       fl &= fl - 1;
@@ -707,19 +732,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       float xg;
       coop_scan<MA, MUSIC>(rds, cfr, crc, ch * 64 + src, A, plane, fstride, G, steer64, xi, xg);
       if (lane == src) {
-        bidx = xi;
-        gval = xg;
+        out_idx[c] = xi;
+        if (out_gmax) out_gmax[c] = xg;
       }
-    }
-    pend = true;
-    pidx = bidx;
-    pgv = gval;
-  }
-  if (pend) {
-    const long long cp = (ch - stride) * 64 + lane;
-    if (cp < ncell) {
-      out_idx[cp] = pidx;
-      if constexpr (GMAX) out_gmax[cp] = pgv;
     }
   }
 }
@@ -770,6 +785,13 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
                      ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,
                      out_spec);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  // the exact re-scan of the marked cells: 256-thread blocks, 4 x 64 cells per block pass, at most 2048 blocks
+  long long fb = (ncell_host + 255) / 256;
+  if (fb > 2048) fb = 2048;
+  if (fb < 1) fb = 1;
+  hipLaunchKernelGGL((k_doa_fixup<MA, MUSIC>), dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
+                     ncell_dev, ncell_host, G, steer64, out_idx, out_gmax);
   return hipGetLastError();
 }
 

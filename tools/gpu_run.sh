@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-4 GPU session driver: each step under its own time limit; a step that times out, aborts or faults
+# (exit 124 / 134 / 137 / 139) ends the session (nothing more runs on the GPU), a failing test does not.
+# usage: bash tools/gpu_run.sh TAG step...   steps: tests | diag | bench | doactr | prof | smoke
+set -u
+TAG=$1; shift
+mkdir -p gpurun_out
+stop() { echo "step $1 ended with $2: stopping"; exit $2; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/${TAG}_${name}.log" 2>&1
+  local rc=$?
+  echo "$name rc $rc"
+  case $rc in 124|134|137|139) stop "$name" $rc;; esac
+}
+for step in "$@"; do
+  case $step in
+    tests) run tests 560 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread ;;
+    smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    diag)
+      for i in 1 2 3 4 5 6; do run diag_ng$i 90 python -u tools/pipelined_repeat.py 2 noguard; done
+      for i in 1 2; do run diag_g$i 90 python -u tools/pipelined_repeat.py 2; done
+      grep -h "mismatching\|placement" gpurun_out/${TAG}_diag_*.log ;;
+    bench) run bench 400 python -u bench.py ;;
+    benchq) run benchq 300 python -u bench.py --no-cpu-baseline --no-pcie --no-extra ;;
+    doactr) F=1000 REPS=3 run doactr 400 bash tools/doa_counters.sh ;;
+    prof) run prof 900 bash tools/profile.sh "$TAG" ;;
+  esac
+done
