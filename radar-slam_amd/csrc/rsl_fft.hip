@@ -368,7 +368,7 @@ RSL_DEV float2 w32(int k) {                // exp(-2 pi i k / 32), k < 16
   return make_float2(c[k], c[(k + 8) & 15] * (k < 8 ? 1.f : -1.f));  // -sin(2 pi k / 32)
 }
 
-template <bool DYN, int DBG = 0>
+template <bool DYN, int DBG = 0, bool NTW = true>
 __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                               int C, long ntile, const float2* __restrict__ table,
                                                               const float2* __restrict__ tw, int dc,
@@ -495,8 +495,8 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile) + tid;
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
-      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
-      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
+      st16<NTW>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
+      st16<NTW>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
     }
     if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
     __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
@@ -1102,6 +1102,10 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       }
     }
 #ifdef RSL_DEV_KNOBS
+    if constexpr (S == 512 && CB == 8) {  // RSL_WORK_TEMPORAL=1: the packed `work` stored without the nt hint (MALL study)
+      if (const char* e = getenv("RSL_WORK_TEMPORAL"))
+        if (wexp && atoi(e) == 1) kern = k_range_fft_r512<true, 0, false>;
+    }
     if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
       const int v = atoi(e);
       if constexpr (S == 512 && CB == 8) {

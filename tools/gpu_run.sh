@@ -25,5 +25,8 @@ for step in "$@"; do
     benchq) run benchq 300 python -u bench.py --no-cpu-baseline --no-pcie --no-extra ;;
     doactr) F=1000 REPS=3 run doactr 400 bash tools/doa_counters.sh ;;
     prof) run prof 900 bash tools/profile.sh "$TAG" ;;
+    mall)
+      RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
+      RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_TEMPORAL=1 run mall_tmp 240 python -u tools/chunk_mall2.py ;;
   esac
 done
