@@ -7,13 +7,21 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-RSL_DEV float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-RSL_DEV float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Complex arithmetic on the 2-wide vector inside float2 (an aligned 64-bit register pair): the compiler emits one
+// v_pk_add_f32 per complex add and v_pk_mul_f32 + v_pk_fma_f32 (with operand swizzles) per complex multiply, instead of
+// scalar ops plus the register-pair shuffles its SLP vectoriser added around the scalar form.  Same roundings:
+// re = fma(a.x, b.x, -(a.y b.y)), im = fma(a.x, b.y, a.y b.x).
+typedef float rsl_f2v __attribute__((ext_vector_type(2)));
+RSL_DEV rsl_f2v cv(float2 a) { return __builtin_bit_cast(rsl_f2v, a); }
+RSL_DEV float2 cf(rsl_f2v v) { return __builtin_bit_cast(float2, v); }
+RSL_DEV float2 cadd(float2 a, float2 b) { return cf(cv(a) + cv(b)); }
+RSL_DEV float2 csub(float2 a, float2 b) { return cf(cv(a) - cv(b)); }
 RSL_DEV float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+  const rsl_f2v va = cv(a), vb = cv(b);
+  return cf(__builtin_elementwise_fma(va.yy, (rsl_f2v){-vb.y, vb.x}, va.xx * vb));
 }
 // multiply by -i : (x + iy)(-i) = y - ix
-RSL_DEV float2 cmul_mi(float2 a) { return make_float2(a.y, -a.x); }
+RSL_DEV float2 cmul_mi(float2 a) { return cf(cv(a).yx * (rsl_f2v){1.f, -1.f}); }
 RSL_DEV float cabs2(float2 a) { return fmaf(a.x, a.x, a.y * a.y); }
 
 // ------------------------------------------------------------------------------------

@@ -440,16 +440,18 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
     Dft<16>::run(v);
+    // lane h = 0 holds E[k], lane h = 1 holds O[k]: u = E[k] or W32^k O[k], swapped with the partner lane by DPP;
+    // bin k1 + 16 k = E + W O on h = 0 (u + recv), bin k1 + 16 (k + 16) = E - W O on h = 1 (recv - u): one packed
+    // fma with a per-lane sign (+1 / -1) instead of selecting operands and both sums
     float2 xo[16];
+    const rsl_f2v sgn = h ? (rsl_f2v){-1.f, -1.f} : (rsl_f2v){1.f, 1.f};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const float2 t2 = cmul(v[k], w32(k));  // W32^k O[k] (used by the h = 1 lane)
-      const float2 send = h ? t2 : v[k];
+      const float2 u = h ? cmul(v[k], w32(k)) : v[k];
       float2 recv;
-      recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, true));
-      recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, true));
-      const float2 a = h ? recv : v[k], b = h ? t2 : recv;  // a = E[k], b = W32^k O[k]
-      xo[k] = h ? csub(a, b) : cadd(a, b);                    // bin k1 + 16 (k + 16 h)
+      recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0xB1, 0xF, 0xF, true));
+      recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0xB1, 0xF, 0xF, true));
+      xo[k] = cf(__builtin_elementwise_fma(sgn, cv(u), cv(recv)));
     }
     if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
     __syncthreads();  // xbuf reads done: obuf aliases it

@@ -25,6 +25,12 @@ for step in "$@"; do
     benchq) run benchq 300 python -u bench.py --no-cpu-baseline --no-pcie --no-extra ;;
     doactr) F=1000 REPS=3 run doactr 400 bash tools/doa_counters.sh ;;
     prof) run prof 900 bash tools/profile.sh "$TAG" ;;
+    ab)  # product library vs radar-slam_amd/lib/librsl_ab.so (tools/build_ab.sh), 2 rounds, one box
+      for r in 1 2; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run ab_old$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+        run ab_new$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_ab_*.log ;;
     mall)
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_TEMPORAL=1 run mall_tmp 240 python -u tools/chunk_mall2.py ;;
