@@ -112,17 +112,22 @@ RSL_DEV void pk_unpack16(const uint4 (&w)[3], float (&f)[16]) {
   const int e = (int)(signed char)((d[2] >> 28) | ((d[5] >> 28) << 4));
   const float s = pk_pow2(e - 22);
   const float off = -kPkMagic * s;
+  const rsl_f2v s2 = {s, s}, o2 = {off, off};
+  // (field & 0x7FFFFF) | 0x4B000000 as one bit-field insert; the two fields of a complex value decoded by one packed fma
+  auto m = [](unsigned x) { return __uint_as_float(__builtin_amdgcn_ubfe(x, 0, 23) | 0x4B000000u); };
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const unsigned u0 = d[3 * g] & 0x7FFFFFu;
-    const unsigned u1 = __builtin_amdgcn_alignbit(d[3 * g + 1], d[3 * g], 23) & 0x7FFFFFu;
-    const unsigned u2 = __builtin_amdgcn_alignbit(d[3 * g + 2], d[3 * g + 1], 14) & 0x7FFFFFu;
-    const unsigned u3 = (d[3 * g + 2] >> 5) & 0x7FFFFFu;
+    const unsigned u0 = d[3 * g];
+    const unsigned u1 = __builtin_amdgcn_alignbit(d[3 * g + 1], d[3 * g], 23);
+    const unsigned u2 = __builtin_amdgcn_alignbit(d[3 * g + 2], d[3 * g + 1], 14);
+    const unsigned u3 = d[3 * g + 2] >> 5;
     // 0x4B000000 | u = 2^23 + u = 1.5 2^23 + n exactly; (that - 1.5 2^23) s in one rounding (exact: n s)
-    f[4 * g] = fmaf(__uint_as_float(0x4B000000u | u0), s, off);
-    f[4 * g + 1] = fmaf(__uint_as_float(0x4B000000u | u1), s, off);
-    f[4 * g + 2] = fmaf(__uint_as_float(0x4B000000u | u2), s, off);
-    f[4 * g + 3] = fmaf(__uint_as_float(0x4B000000u | u3), s, off);
+    const rsl_f2v a = __builtin_elementwise_fma((rsl_f2v){m(u0), m(u1)}, s2, o2);
+    const rsl_f2v b = __builtin_elementwise_fma((rsl_f2v){m(u2), m(u3)}, s2, o2);
+    f[4 * g] = a.x;
+    f[4 * g + 1] = a.y;
+    f[4 * g + 2] = b.x;
+    f[4 * g + 3] = b.y;
   }
 }
 
