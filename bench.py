@@ -447,7 +447,8 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     import torch
     import torch.distributed as dist
     import rsl
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=ridge)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=ridge,
+                          front_chunk=int(os.environ.get('RSL_BENCH_FRONT_CHUNK', '0')))
     NS = max(1, streams)
     if F % NS:
         raise SystemExit('--frames-per-step must be a multiple of --streams')
@@ -574,7 +575,8 @@ def chain_rooflines(r, A, C, S, F, config):
                  else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
     per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
     flops = 3 * 2 * (2 * A - 1) * ncl * G
-    kbytes = kernel_bytes_k1k2(A, C, S, Fl)
+    Ff = min(Fl, r['chains'][0].chunk)  # frames per K1 / K2 launch (ChainConfig.front_chunk)
+    kbytes = kernel_bytes_k1k2(A, C, S, Ff)
 
     def entry(name, ms):
         if name == 'doa_scan':
@@ -587,7 +589,7 @@ def chain_rooflines(r, A, C, S, F, config):
         kern = fft_names[name]
         ach = kbytes[name] / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Fl, config),
+                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Ff, config),
                 "traffic_source": TRAFFIC_SOURCE, "avg_launch_ms": ms, "design_bytes_per_launch": kbytes[name],
                 "note": "per-kernel design bytes (cube or work in, work or RDS out): the work round trip counts "
                         "here, so these fractions are kernel efficiencies, not the stage's algorithmic roofline"}
@@ -599,11 +601,11 @@ def chain_rooflines(r, A, C, S, F, config):
     # algorithmic bytes.
     big = ('range_fft', 'doppler_fft', 'doa_scan')
     fft_k = [k for k in ('range_fft', 'doppler_fft') if k in kt and kt[k][1]]
-    fft_bytes = 2 * A * C * S * 8 * Fl
+    fft_bytes = 2 * A * C * S * 8 * Ff
 
     def stage(src, timed):
         t = sum(src[k][0] / max(src[k][1], 1) for k in fft_k) * 1e-3
-        tr = [pmc_traffic(fft_names[k], Fl, config) for k in fft_k]
+        tr = [pmc_traffic(fft_names[k], Ff, config) for k in fft_k]
         return {"bound": "hbm", "kernels": [fft_names[k] for k in fft_k],
                 "achieved": fft_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": fft_bytes / t / 1e9 / HBM_PEAK_GBS,
@@ -616,7 +618,10 @@ def chain_rooflines(r, A, C, S, F, config):
         out["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
     out["roofline_doa"] = entry('doa_scan', per('doa_scan'))
     out["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big if k in src_std}
-    out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * NS for k, v in kt.items() if v[1]}
+    out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * (NS if k not in fft_names else Fl * NS / Ff)
+                                 for k, v in kt.items() if v[1]}
+    if Ff < Fl:
+        out["front_chunk_frames"] = Ff
     if ks:
         out["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
     return out

@@ -31,6 +31,9 @@ for step in "$@"; do
         run ab_new$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab_*.log ;;
+    chunk)  # the chained front half in chunks of N frames (ChainConfig.front_chunk), product nt work stores
+      for n in 0 32 64; do RSL_BENCH_FRONT_CHUNK=$n run chunk$n 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_chunk*.log ;;
     mall)
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_TEMPORAL=1 run mall_tmp 240 python -u tools/chunk_mall2.py ;;
