@@ -32,7 +32,7 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab_*.log ;;
     chunk)  # the chained front half in chunks of N frames (ChainConfig.front_chunk), product nt work stores
-      for n in 0 32 64; do RSL_BENCH_FRONT_CHUNK=$n run chunk$n 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
+      for n in 0 16 32; do RSL_BENCH_FRONT_CHUNK=$n run chunk$n 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_chunk*.log ;;
     mall)
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
