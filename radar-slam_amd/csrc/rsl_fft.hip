@@ -87,12 +87,15 @@ RSL_DEV float pk_pow2(int k) { return __uint_as_float((unsigned)(127 + k) << 23)
 // of the int8 e, x_2 = x_3 = 0
 RSL_DEV void pk_pack16(const float (&f)[16], int e, uint4 (&o)[3]) {
   const float s = pk_pow2(22 - e);
+  const rsl_f2v s2 = {s, s}, mg = {kPkMagic, kPkMagic};
   unsigned u[16], d[12];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    // fma rounds v s to the nearest integer (|v s| < 2^22); the min keeps a value that rounds up to 2^22 in range
-    const unsigned b = min(__float_as_uint(fmaf(f[c], s, kPkMagic)), 0x4B7FFFFFu);
-    u[c] = b & 0x7FFFFFu;
+  for (int c = 0; c < 16; c += 2) {
+    // fma rounds v s to the nearest integer (|v s| < 2^22; one packed fma per complex value); the min keeps a value
+    // that rounds up to 2^22 in range
+    const rsl_f2v q = __builtin_elementwise_fma((rsl_f2v){f[c], f[c + 1]}, s2, mg);
+    u[c] = min(__float_as_uint(q.x), 0x4B7FFFFFu) & 0x7FFFFFu;
+    u[c + 1] = min(__float_as_uint(q.y), 0x4B7FFFFFu) & 0x7FFFFFu;
   }
   const unsigned eb = (unsigned)e & 0xFFu;
 #pragma unroll
