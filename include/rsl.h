@@ -100,6 +100,16 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
                    void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group);
 
+/* rsl_rds_detect over the batch in chunks of chunk_frames frames (the last one shorter) through one chunk-sized work
+ *     buffer: K1 -> K2 of each chunk back to back on the handle's stream, so that a chunk's range spectra (packed
+ *     `work`, stored without the nt hint when a launch's `work` is <= 128 MiB) can be read from the 256 MiB Infinity
+ *     Cache instead of HBM.  work must hold chunk_frames frames; every other argument and output as rsl_rds_detect
+ *     (outputs bit-identical to it).  chunk_frames <= 0 or >= F: one rsl_rds_detect call. */
+int rsl_rds_detect_chunked(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
+                           const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo,
+                           int i_hi, void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group,
+                           int chunk_frames);
+
 /* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
  * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
  *     entry_row_off i32 [F*A*S], cell_row_off i32 [F*S], scratch i32 [F*S],

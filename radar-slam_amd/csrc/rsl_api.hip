@@ -246,6 +246,31 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   return hip_check(h, e, "doppler_detect");
 }
 
+int rsl_rds_detect_chunked(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
+                           const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo,
+                           int i_hi, void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group,
+                           int chunk_frames) {
+  if (!h) return RSL_ERR_INVALID;
+  if (chunk_frames <= 0 || chunk_frames >= F)
+    return rsl_rds_detect(h, cube, F, A, C_total, chirp0, C, S, table, dc_removal, work, rds, thr_power, i_lo, i_hi,
+                          mask, row_count, db_map, peak_pow, peak_pow_group);
+  if (A <= 0 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect_chunked: bad shape");
+  const int W = (C + 63) / 64;
+  const size_t per_cube = (size_t)A * C_total * S * sizeof(float2), per_rds = (size_t)A * S * C * sizeof(float2);
+  const size_t per_mask = (size_t)A * S * W * 8, per_rc = (size_t)A * S * 4, per_map = (size_t)A * S * C * 4;
+  for (int f0 = 0; f0 < F; f0 += chunk_frames) {
+    const int n = F - f0 < chunk_frames ? F - f0 : chunk_frames;
+    auto at = [&](const void* p, size_t per) -> void* {
+      return p ? (void*)((const unsigned char*)p + per * (size_t)f0) : nullptr;
+    };
+    if (int r = rsl_rds_detect(h, at(cube, per_cube), n, A, C_total, chirp0, C, S, table, dc_removal, work,
+                               at(rds, per_rds), thr_power, i_lo, i_hi, at(mask, per_mask), at(row_count, per_rc),
+                               at(db_map, per_map), at(peak_pow, per_map), peak_pow_group))
+      return r;
+  }
+  return RSL_OK;
+}
+
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
                void* mask, void* row_count, void* db_map, void* peak_pow) {
   if (!h) return RSL_ERR_INVALID;

@@ -149,12 +149,9 @@ class RadarChain:
         if self.F == 0:  # empty batch: only the (zeroed) bases
             ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
             return
-        n = self.chunk
-        for f0 in range(0, self.F, n):
-            f1 = min(self.F, f0 + n)
-            group = ctx.rds_detect(cube[f0:f1], self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds[f0:f1],
-                                   work=self.work[:f1 - f0], mask=self.mask[f0:f1], row_count=self.row_count[f0:f1],
-                                   peak_pow=self.peak_pow[f0:f1], dc_removal=cfg.dc_removal)
+        group = ctx.rds_detect(cube, self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds, work=self.work,
+                               mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow,
+                               dc_removal=cfg.dc_removal, chunk=self.chunk if self.chunk < self.F else 0)
         self._group = group
         if offsets:
             ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)
