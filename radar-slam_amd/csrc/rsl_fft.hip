@@ -1131,7 +1131,16 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       if (!wexp && v == 3) kern = k_range_fft_p<S, CB, true, 3>;
     }
 #endif
-    const long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds_k, ntile);
+    long nblk = resident_grid(reinterpret_cast<const void*>(kern), lds_k, ntile);
+#ifdef RSL_DEV_KNOBS
+    if (const char* e = getenv("RSL_K1_WG_PER_CU")) {  // fewer resident K1 workgroups (room for the other stream)
+      int dev = 0, ncu = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      const long cap = (long)atoi(e) * ncu;
+      if (cap >= 8 && cap < nblk) nblk = cap;
+    }
+#endif
     int slot = 0;
     if (nblk >= 8) {  // the per-XCD dequeue needs a workgroup on every XCD
       static std::atomic<int> next_slot{0};

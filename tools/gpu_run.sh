@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session driver: each step under its own time limit; a step that times out, aborts or faults
 # (exit 124 / 134 / 137 / 139) ends the session (nothing more runs on the GPU), a failing test does not.
-# usage: bash tools/gpu_run.sh TAG step...   steps: tests | diag | bench | doactr | prof | smoke
+# usage: bash tools/gpu_run.sh TAG step...   steps: tests | smoke | diag | bench | benchq | doactr | prof | ab | chunk | k1cap | mall
 set -u
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -34,6 +34,11 @@ for step in "$@"; do
     chunk)  # the chained front half in chunks of N frames (ChainConfig.front_chunk), product nt work stores
       for n in 0 16 32; do RSL_BENCH_FRONT_CHUNK=$n run chunk$n 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_chunk*.log ;;
+    k1cap)  # resident K1 workgroups per CU capped (dev library, RSL_K1_WG_PER_CU): room for the back stream
+      for r in 1 2; do
+        for n in 0 2; do RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_K1_WG_PER_CU=$n run k1cap${n}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_k1cap*.log ;;
     mall)
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
       RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_TEMPORAL=1 run mall_tmp 240 python -u tools/chunk_mall2.py ;;
