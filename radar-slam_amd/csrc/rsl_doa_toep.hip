@@ -250,9 +250,16 @@ RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
 // round-3 build made had gaps <= 8.6e-8).  ~0.2 % of cfg2 cells fall inside the bound.
 constexpr float kAmbRel = 2e-6f;
 
+// Ties of the exact scan: keys within this relative distance count as equal and the lower grid index wins, as
+// np.argmax does on an exact tie.  Such keys are equal in exact arithmetic up to fp64 rounding (the reference's own
+// fp64 noise decides between them, e.g. the identical steering vectors of -90 and +90 degrees at d = lambda / 2),
+// and the parity tests treat gaps <= 1e-12 as ties (tests/parity.py OWN_TIE_RGAP).
+constexpr double kTieRel = 1e-12;
+
 // Exact fp64 scan of ONE cell by the whole wave (lanes split the grid points; wave-uniform cell c): the key is P if
 // M - P > 1e-12 (MUSIC, angle_estimation.py:149-152) else -1, P for beamforming; first index of the maximum key, as
-// np.argmax.  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table.  Returns (index, P at it) on every lane.
+// np.argmax (ties within kTieRel).  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table.  Returns
+// (index, P at it) on every lane.
 template <int MA, bool MUSIC>
 RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
                        long long c, int A, size_t plane, size_t fstride, int G, const double* __restrict__ steer64,
@@ -272,10 +279,10 @@ RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ c
   }
   const double sc = pw > 0.0 ? 1.0 / sqrt(pw) : 1.0;
   const int lane = threadIdx.x & 63;
-  double best = -INFINITY, bp = 0.0;
+  double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
   int bi = G;
-#pragma unroll 1
-  for (int g = lane; g < G; g += 64) {  // ascending g per lane: strict '>' keeps the first index
+#pragma unroll 3
+  for (int g = lane; g < G; g += 64) {  // ascending g per lane: a later g must beat the tie tolerance
     const double* a = steer64 + (size_t)g * A * 2;
     double zr = 0.0, zi = 0.0;
 #pragma unroll 2
@@ -287,19 +294,20 @@ RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ c
     }
     const double p = (zr * zr + zi * zi) * sc * sc;
     const double key = MUSIC ? (((double)A - p > 1e-12) ? p : -1.0) : p;
-    if (key > best) {
+    if (key > best + kTieRel * fabs(best)) {
       best = key;
       bi = g;
       bp = p;
     }
   }
-  // wave argmax of (key, index): larger key, then lower index
+  // wave argmax of (key, index): larger key beyond the tie tolerance, else lower index
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const double ok = __shfl_xor(best, off);
     const int oi = __shfl_xor(bi, off);
     const double op = __shfl_xor(bp, off);
-    if (ok > best || (ok == best && oi < bi)) {
+    const double tol = kTieRel * fmax(fabs(ok), fabs(best));
+    if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
       best = ok;
       bi = oi;
       bp = op;
@@ -710,7 +718,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
 
 // Exact fp64 argmax of the cells k_doa_toep marked ambiguous (out_idx < 0: its f16 top-2 gap was inside kAmbRel, or a
 // MUSIC maximum within rounding of M): each wave reads 64 consecutive indices, and every marked cell is re-scanned by
-// the whole wave (coop_scan: lanes split the grid points).  Grid-stride over the cells; ~0.2 % of cfg2 cells.
+// the whole wave (coop_scan: lanes split the grid points).  One wave per 64 cells, all in parallel (a grid-stride
+// loop chained one index load per chunk: ~135 dependent round trips per wave at 2000 cfg2 frames).
 template <int MA, bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
@@ -786,10 +795,13 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
                      ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,
                      out_spec);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  // the exact re-scan of the marked cells: 256-thread blocks, 4 x 64 cells per block pass, at most 2048 blocks
+  // the exact re-scan of the marked cells: 256-thread blocks, one wave per 64 cells
   long long fb = (ncell_host + 255) / 256;
-  if (fb > 2048) fb = 2048;
   if (fb < 1) fb = 1;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - index
+    if (atoi(e) == 1) return hipSuccess;
+#endif
   hipLaunchKernelGGL((k_doa_fixup<MA, MUSIC>), dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
                      ncell_dev, ncell_host, G, steer64, out_idx, out_gmax);
   return hipGetLastError();

@@ -123,11 +123,18 @@ class Context:
         C = Ct - chirp0 if num_chirps is None else num_chirps
         group = ctypes.c_int(1)
         self._bind()
-        self.check(self.lib.rsl_rds_detect_chunked(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
-                                                   int(dc_removal), _ptr(work), _ptr(rds), float(thr_power), int(i_lo),
-                                                   int(i_hi), _ptr(mask), _ptr(row_count), _ptr(db_map),
-                                                   _ptr(peak_pow), ctypes.byref(group), int(chunk)),
-                   'rsl_rds_detect')
+        if 0 < chunk < F:
+            self.check(self.lib.rsl_rds_detect_chunked(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
+                                                       int(dc_removal), _ptr(work), _ptr(rds), float(thr_power),
+                                                       int(i_lo), int(i_hi), _ptr(mask), _ptr(row_count),
+                                                       _ptr(db_map), _ptr(peak_pow), ctypes.byref(group), int(chunk)),
+                       'rsl_rds_detect_chunked')
+        else:
+            self.check(self.lib.rsl_rds_detect(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
+                                               int(dc_removal), _ptr(work), _ptr(rds), float(thr_power), int(i_lo),
+                                               int(i_hi), _ptr(mask), _ptr(row_count), _ptr(db_map), _ptr(peak_pow),
+                                               ctypes.byref(group)),
+                       'rsl_rds_detect')
         return int(group.value)
 
     # -- a8 -------------------------------------------------------------------------------------

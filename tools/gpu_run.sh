@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session driver: each step under its own time limit; a step that times out, aborts or faults
 # (exit 124 / 134 / 137 / 139) ends the session (nothing more runs on the GPU), a failing test does not.
-# usage: bash tools/gpu_run.sh TAG step...   steps: tests | smoke | diag | bench | benchq | doactr | prof | ab | chunk | k1cap | mall
+# usage: bash tools/gpu_run.sh TAG step...   steps: tests | testsall | fixcount | smoke | diag | bench | benchq | doactr | prof | ab | chunk | k1cap | mall
 set -u
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -16,6 +16,8 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     tests) run tests 560 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread ;;
+    testsall) run testsall 600 python -u -m pytest tests -m gpu -q --maxfail 12 --timeout 150 --timeout-method thread ;;
+    fixcount) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fixcount 200 python -u tools/doa_fix_count.py ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     diag)
       for i in 1 2 3 4 5 6; do run diag_ng$i 90 python -u tools/pipelined_repeat.py 2 noguard; done
