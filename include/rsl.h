@@ -148,8 +148,9 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
  *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = min(*ncell_dev, ncell) if ncell_dev is non-null
  *     (ncell = the lists' capacity: an overflowed list is processed up to its capacity), else ncell.
  *     steer_tab = device copy of the rsl_steer_table_build output; steer_c128 = device fp64 [G][M][2]
- *     steering matrix (needed with RSL_DOA_TOEPLITZ: the exact fp64 re-scan of the cells whose f16 hi/lo top-2 gap
- *     is inside the scan's error bound, and of MUSIC's near-degenerate cells, so out_idx is the fp64 argmax).
+ *     steering matrix (required: the exact fp64 re-scan of the cells whose top-2 gap in the f16 hi/lo or f32 scan
+ *     is inside that scan's error bound, and of MUSIC's near-degenerate cells, so out_idx is the fp64 argmax of each
+ *     cell's own signature; keys within 1e-12 relative count as ties and the lower index wins, as np.argmax).
  *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; with out_spec it applies to the RSL_DOA_SPEC_BLOCKED layout
  *     without out_gmax, the other spectrum requests take the f32 scan).
  *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
@@ -162,7 +163,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
 
 /* a11-a16 + a15 + a26 fused: the Toeplitz argmax of rsl_doa (requires RSL_STEER_TOEPLITZ) plus, from the same
  *     signature load, ESPRIT (f64 deg, nullable; angle_estimation.py:178-225, esprit_scale = lambda/(2 pi d))
- *     (steer_c128 required, as for the Toeplitz rsl_doa)
+ *     (steer_c128 required, as for rsl_doa)
  *     and the spatial phase angle(s1 conj(s0)) (f64, nullable; velocity_solver.py:136) of each cell.
  *     Returns RSL_ERR_UNSUPPORTED when the grid does not fit the Toeplitz path. */
 int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,

@@ -402,8 +402,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   if (base_method != RSL_METHOD_MUSIC && base_method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
   const bool music = base_method == RSL_METHOD_MUSIC;
-  if (toep && !steer_c128)
-    return fail(h, RSL_ERR_INVALID, "rsl_doa: the Toeplitz path needs the fp64 steering table (exact re-scan)");
+  if (!steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa: needs the fp64 steering table (exact re-scan)");
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
   Scope sc(h, RSL_K_DOA_SCAN);
@@ -423,13 +422,22 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   long long blocks = 0;  // 0: all resident workgroups (occupancy x CUs)
   if (!ncell_dev) blocks = (ncell + 127) / 128;  // 4 waves x 32 cells
   const int ntiles = (2 * G + 15) / 16;
+  if (int r = hip_check(h,
+                        rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
+                                             (const int*)c_rc, (const long long*)ncell_dev, ncell,
+                                             (const float*)steer_tab, ntiles, G, music, (int*)out_idx,
+                                             (float*)out_gmax, (float*)out_spec,
+                                             (method & RSL_DOA_SPEC_BLOCKED) ? -1
+                                             : (method & RSL_DOA_SPEC_GMAJOR) ? ncell : 0,
+                                             (int)blocks),
+                        "doa_scan"))
+    return r;
+  // the cells the f32 scan marked ambiguous: exact fp64 argmax (rsl_doa_toep.hip k_doa_fixup)
   return hip_check(h,
-                   rsl::launch_doa_scan(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
-                                        (const long long*)ncell_dev, ncell, (const float*)steer_tab, ntiles, G,
-                                        music, (int*)out_idx, (float*)out_gmax, (float*)out_spec,
-                                        (method & RSL_DOA_SPEC_BLOCKED) ? -1 : (method & RSL_DOA_SPEC_GMAJOR) ? ncell : 0,
-                                        (int)blocks),
-                   "doa_scan");
+                   rsl::launch_doa_fixup(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
+                                         (const int*)c_rc, (const long long*)ncell_dev, ncell, G, music,
+                                         (const double*)steer_c128, (int*)out_idx, (float*)out_gmax),
+                   "doa_fixup");
 }
 
 int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,

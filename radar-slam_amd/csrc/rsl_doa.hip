@@ -52,6 +52,19 @@ RSL_DEV void load_sig(const float2* __restrict__ rds, const int* __restrict__ cf
   }
 }
 
+// Ambiguity bound of the f32 scans (relative top-2 gap): the [Re; Im] products are exact fp32 fmaf chains of <= 32
+// terms, so P = re^2 + im^2 is within a few fp32 ulps of the fp64 value of the same fp32 signature; a cell whose
+// best grid value is not this far above every other one (or, MUSIC, whose maximum is within rounding of M, where
+// the reference's den > 1e-12 rule may move the argmax) is marked -1 - (g | 1 << 24) and re-scanned over the whole
+// grid in fp64 by k_doa_fixup (rsl_doa_toep.hip), so that no grid index differs from the fp64 argmax of the cell's
+// own signature by the scan's rounding.
+constexpr float kAmbRel32 = 4e-6f;
+
+RSL_DEV int mark_amb(int g, float best, float second, bool music, float Mf) {
+  const bool amb = second >= best * (1.f - kAmbRel32) || !(best > 0.f) || (music && best >= Mf - 1e-4f);
+  return amb ? -1 - (g | (1 << 24)) : g;
+}
+
 // One wave = 32 cells (two 16-column MFMA tiles) per pass over all grid tiles; the next pass's signature
 // loads are issued before the current pass's MFMAs (software prefetch).  Grid = resident workgroups only
 // (occupancy query), grid-striding over 32-cell chunks, so no tail wave of late workgroups.
@@ -118,7 +131,7 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
         load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
       }
     }
-    float best[2] = {-INFINITY, -INFINITY};
+    float best[2] = {-INFINITY, -INFINITY}, second[2] = {-INFINITY, -INFINITY};
     float bestg[2] = {0.f, 0.f};
     int bidx[2] = {0, 0};
     for (int t = 0; t < ntiles; ++t) {
@@ -148,10 +161,15 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
           const float gv = fmaf(re, re, im * im);
           float key = gv;
           if constexpr (MUSIC) key = (Mf - gv > 1e-12f) ? gv : -1.f;  // den <= 1e-12 -> spectrum 0
-          if (key > best[t2] && g < G) {
-            best[t2] = key;
-            bidx[t2] = g;
-            if constexpr (GMAX) bestg[t2] = gv;
+          if (g < G) {
+            if (key > best[t2]) {
+              second[t2] = best[t2];
+              best[t2] = key;
+              bidx[t2] = g;
+              if constexpr (GMAX) bestg[t2] = gv;
+            } else {
+              second[t2] = fmaxf(second[t2], key);
+            }
           }
           if constexpr (SPEC) {
             float val = gv;
@@ -197,18 +215,20 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
     for (int t2 = 0; t2 < 2; ++t2) {
 #pragma unroll
       for (int off = 16; off <= 32; off <<= 1) {
-        const float ob = __shfl_xor(best[t2], off);
+        const float ob = __shfl_xor(best[t2], off), os = __shfl_xor(second[t2], off);
         const int oi = __shfl_xor(bidx[t2], off);
         float og = 0.f;
         if constexpr (GMAX) og = __shfl_xor(bestg[t2], off);
-        if (ob > best[t2] || (ob == best[t2] && oi < bidx[t2])) {  // first index wins (np.argmax)
+        const bool take = ob > best[t2] || (ob == best[t2] && oi < bidx[t2]);  // first index wins (np.argmax)
+        second[t2] = fmaxf(fmaxf(second[t2], os), take ? best[t2] : ob);
+        if (take) {
           best[t2] = ob;
           bidx[t2] = oi;
           if constexpr (GMAX) bestg[t2] = og;
         }
       }
       if (q == 0 && ok[t2]) {
-        out_idx[cidx[t2]] = bidx[t2];
+        out_idx[cidx[t2]] = mark_amb(bidx[t2], best[t2], second[t2], MUSIC, Mf);
         if constexpr (GMAX) out_gmax[cidx[t2]] = bestg[t2];
       }
     }
@@ -224,11 +244,12 @@ __global__ __launch_bounds__(256) void k_doa_scan(const float2* __restrict__ rds
 // NCT = 16-cell column tiles per wave (independent MFMA accumulator chains).
 template <int KS, bool FAST, int NCT, bool KEYED>
 RSL_DEV void argmax_scan(const float4* __restrict__ st, int ntiles, int G, float Mf, int q,
-                         const float (&b)[NCT][KS], float (&best)[NCT], int (&bidx)[NCT]) {
+                         const float (&b)[NCT][KS], float (&best)[NCT], float (&second)[NCT], int (&bidx)[NCT]) {
   constexpr int KSG = (KS + 3) / 4;
 #pragma unroll
   for (int t2 = 0; t2 < NCT; ++t2) {
     best[t2] = -INFINITY;
+    second[t2] = -INFINITY;
     bidx[t2] = 0;
   }
 #pragma unroll 2
@@ -264,9 +285,10 @@ RSL_DEV void argmax_scan(const float4* __restrict__ st, int ntiles, int G, float
         if (i0 + 1 >= G) g1 = -INFINITY;
       }
       const bool c = g1 > g0;
-      const float m = c ? g1 : g0;
+      const float m = c ? g1 : g0, lo = c ? g0 : g1;
       const int ii = c ? i0 + 1 : i0;
       const bool u = m > best[t2];
+      second[t2] = u ? fmaxf(best[t2], lo) : fmaxf(second[t2], m);  // top-2 of everything this lane has seen
       best[t2] = u ? m : best[t2];
       bidx[t2] = u ? ii : bidx[t2];
     }
@@ -328,28 +350,29 @@ __global__ __launch_bounds__(256) void k_doa_argmax(const float2* __restrict__ r
         load_sig<KS, FAST>(rds, cfr, crc, c, c < ncell, A, q, plane, fstride, nb[t2]);
       }
     }
-    float best[NCT];
+    float best[NCT], second[NCT];
     int bidx[NCT];
-    argmax_scan<KS, FAST, NCT, false>(st, ntiles, G, Mf, q, b, best, bidx);
+    argmax_scan<KS, FAST, NCT, false>(st, ntiles, G, Mf, q, b, best, second, bidx);
     if constexpr (MUSIC) {
       bool hit = false;
 #pragma unroll
       for (int t2 = 0; t2 < NCT; ++t2) hit |= !(Mf - best[t2] > 1e-12f);
-      if (__ballot(hit)) argmax_scan<KS, FAST, NCT, true>(st, ntiles, G, Mf, q, b, best, bidx);  // rare
+      if (__ballot(hit)) argmax_scan<KS, FAST, NCT, true>(st, ntiles, G, Mf, q, b, best, second, bidx);  // rare
     }
 #pragma unroll
     for (int t2 = 0; t2 < NCT; ++t2) {
 #pragma unroll
       for (int off = 16; off <= 32; off <<= 1) {
-        const float ob = __shfl_xor(best[t2], off);
+        const float ob = __shfl_xor(best[t2], off), os = __shfl_xor(second[t2], off);
         const int oi = __shfl_xor(bidx[t2], off);
         const bool take = (ob > best[t2]) | ((ob == best[t2]) & (oi < bidx[t2]));  // first index wins
+        second[t2] = fmaxf(fmaxf(second[t2], os), take ? best[t2] : ob);
         best[t2] = take ? ob : best[t2];
         bidx[t2] = take ? oi : bidx[t2];
       }
       const long long c = ch * CPW + t2 * 16 + jj;
       if (q == 0 && c < ncell) {
-        out_idx[c] = bidx[t2];
+        out_idx[c] = mark_amb(bidx[t2], best[t2], second[t2], MUSIC, Mf);
         if constexpr (GMAX) out_gmax[c] = best[t2];
       }
     }

@@ -256,53 +256,66 @@ constexpr float kAmbRel = 2e-6f;
 // and the parity tests treat gaps <= 1e-12 as ties (tests/parity.py OWN_TIE_RGAP).
 constexpr double kTieRel = 1e-12;
 
-// Exact fp64 scan of ONE cell by the whole wave (lanes split the grid points; wave-uniform cell c): the key is P if
+// Exact fp64 scan of ONE cell over grid points [g0, g1) by the whole wave (wave-uniform cell c): the key is P if
 // M - P > 1e-12 (MUSIC, angle_estimation.py:149-152) else -1, P for beamforming; first index of the maximum key, as
-// np.argmax (ties within kTieRel).  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table.  Returns
-// (index, P at it) on every lane.
-template <int MA, bool MUSIC>
+// np.argmax (ties within kTieRel).  P = |a^H s|^2 / |s|^2 from the reference's fp64 steering table [G][A].  Lane =
+// (grid point p = lane >> 3 of 8 per step, antenna m = lane & 7, and m + 8 for A > 8): each steering load is one
+// 16-B complex of a row, so a step's 64 lanes read 8 consecutive rows as contiguous 128-B runs (lanes splitting the
+// grid points with a whole row each read 16 lines per instruction: 16x the L2 requests); the sum over the antennas
+// is three xor shuffles inside the 8-lane group.  Returns (index, P at it) on every lane.
+template <bool MUSIC>
 RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
-                       long long c, int A, size_t plane, size_t fstride, int G, const double* __restrict__ steer64,
-                       int& idx, float& gval) {
-  // the cell's signature in scalar registers (wave-uniform): the rare path adds no vector-register pressure to the
-  // kernel's hot loop (whose 128-VGPR budget sets 4 waves per SIMD)
+                       long long c, int A, size_t plane, size_t fstride, int g0, int g1,
+                       const double2* __restrict__ steer64, int& idx, float& gval) {
+  const int lane = threadIdx.x & 63;
+  const int m = lane & 7, p = lane >> 3;
   const int fx = __builtin_amdgcn_readfirstlane(cfr[c]), fy = __builtin_amdgcn_readfirstlane(crc[c]);
   const float2* base = rds + (size_t)fx * fstride + fy;
-  float sr[MA], si[MA];
-  double pw = 0.0;
-#pragma unroll
-  for (int m = 0; m < MA; ++m) {
-    const float2 z = m < A ? base[(size_t)m * plane] : make_float2(0.f, 0.f);
-    sr[m] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z.x)));
-    si[m] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(z.y)));
-    pw += (double)sr[m] * sr[m] + (double)si[m] * si[m];
-  }
-  const double sc = pw > 0.0 ? 1.0 / sqrt(pw) : 1.0;
-  const int lane = threadIdx.x & 63;
+  const float2 u0 = m < A ? base[(size_t)m * plane] : make_float2(0.f, 0.f);
+  const float2 u1 = m + 8 < A ? base[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
+  const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
+  double pw = x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1);
+  pw += __shfl_xor(pw, 1);
+  pw += __shfl_xor(pw, 2);
+  pw += __shfl_xor(pw, 4);
+  const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
   double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
-  int bi = G;
-#pragma unroll 3
-  for (int g = lane; g < G; g += 64) {  // ascending g per lane: a later g must beat the tie tolerance
-    const double* a = steer64 + (size_t)g * A * 2;
+  int bi = g1;
+  for (int gb = g0; gb < g1; gb += 8) {  // ascending g per 8-lane group: a later g must beat the tie tolerance
+    const int g = gb + p;
     double zr = 0.0, zi = 0.0;
-#pragma unroll 2
-    for (int m = 0; m < A && m < MA; ++m) {
-      const double ar = a[2 * m], ai = a[2 * m + 1];
-      const double xr = sr[m], xi = si[m];
-      zr += ar * xr + ai * xi;
-      zi += ar * xi - ai * xr;
+    if (g < g1) {
+      const double2* row = steer64 + (size_t)g * A;
+      if (m < A) {
+        const double2 a = row[m];
+        zr = a.x * x0 + a.y * y0;  // conj(a) s
+        zi = a.x * y0 - a.y * x0;
+      }
+      if (m + 8 < A) {
+        const double2 a = row[m + 8];
+        zr += a.x * x1 + a.y * y1;
+        zi += a.x * y1 - a.y * x1;
+      }
     }
-    const double p = (zr * zr + zi * zi) * sc * sc;
-    const double key = MUSIC ? (((double)A - p > 1e-12) ? p : -1.0) : p;
-    if (key > best + kTieRel * fabs(best)) {
-      best = key;
-      bi = g;
-      bp = p;
+    zr += __shfl_xor(zr, 1);
+    zi += __shfl_xor(zi, 1);
+    zr += __shfl_xor(zr, 2);
+    zi += __shfl_xor(zi, 2);
+    zr += __shfl_xor(zr, 4);
+    zi += __shfl_xor(zi, 4);
+    if (g < g1) {
+      const double pv = (zr * zr + zi * zi) * sc2;
+      const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
+      if (key > best + kTieRel * fabs(best)) {
+        best = key;
+        bi = g;
+        bp = pv;
+      }
     }
   }
-  // wave argmax of (key, index): larger key beyond the tie tolerance, else lower index
+  // argmax over the 8 groups of (key, index): larger key beyond the tie tolerance, else lower index
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
+  for (int off = 8; off < 64; off <<= 1) {
     const double ok = __shfl_xor(best, off);
     const int oi = __shfl_xor(bi, off);
     const double op = __shfl_xor(bp, off);
@@ -617,11 +630,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         // the running SECOND joins the max tree (same 8 v_max3): m2 = max(second, tile max); since second <= best,
         // m2 > best <=> the tile max > best.  A record moves best to second; otherwise second = m2 (the largest tile
         // maximum of the other tiles: the end-of-pass ambiguity test)
+        // branch-free top-2: a record (m2 > best) leaves second = the old best, otherwise second = m2 -- both are
+        // min(best, m2); best = max(best, m2).  Only the record tile's index and copy sit under the branch.
+        // (integer min / max on the bit patterns, as in tile_max: the values are non-negative, and fminf / fmaxf
+        // would add an IEEE canonicalising v_max per operand)
         const float m2 = tile_max(acc, second);
         const bool r = m2 > best;
-        second = r ? best : m2;
+        const int bb = __float_as_int(best), mb = __float_as_int(m2);
+        second = __int_as_float(min(bb, mb));
+        best = __int_as_float(max(bb, mb));
         if (r) {
-          best = m2;
           set_bt(sh, t);
           if constexpr (DBG != 1) copy_tile(sv, acc);
         }
@@ -663,7 +681,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     // 16 values >= theta, n = how many there are.  n == 1: that value is the lane's maximum and every other value of
     // the lane is below theta, so i is its exact argmax; n >= 2, a tile maximum of another tile >= theta, or a
     // non-positive best (a zero signature): ambiguous, re-scanned in fp64 below.
-    int i0 = 15, i1 = 15, n0 = 0, n1 = 0;
+    // (any / two as lane masks: scalar ALU work, only the compares and the index selects are vector instructions)
+    int i0 = 15, i1 = 15;
+    bool any0 = false, two0 = false, any1 = false, two1 = false;
     {
       const floatx16 r0 = __builtin_bit_cast(floatx16, sv0), r1 = __builtin_bit_cast(floatx16, sv1);
       const float th0 = best0 * (1.f - kAmbRel), th1 = best1 * (1.f - kAmbRel);
@@ -672,20 +692,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         const bool g0 = r0[i] >= th0, g1 = r1[i] >= th1;
         i0 = g0 ? i : i0;
         i1 = g1 ? i : i1;
-        n0 += g0;
-        n1 += g1;
+        two0 = two0 || (any0 && g0);
+        two1 = two1 || (any1 && g1);
+        any0 = any0 || g0;
+        any1 = any1 || g1;
       }
     }
-    bool amb0 = n0 != 1 || second0 >= best0 * (1.f - kAmbRel) || !(best0 > 0.f);
-    bool amb1 = n1 != 1 || second1 >= best1 * (1.f - kAmbRel) || !(best1 > 0.f);
+    bool amb0 = !any0 || two0 || second0 >= best0 * (1.f - kAmbRel) || !(best0 > 0.f);
+    bool amb1 = !any1 || two1 || second1 >= best1 * (1.f - kAmbRel) || !(best1 > 0.f);
     int g0 = 32 * (bt01 & 0xFFFF) + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
     int g1 = 32 * (bt01 >> 16) + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
     // merge the two K-half lanes of each column (first index wins on ties); ambiguous if the winner is, or if the
     // loser's maximum is within the bound of the winner's (an exact tie included)
+    // Window of the exact re-scan: the record tile alone when both K halves recorded in the same tile and no other
+    // tile of either half came within the bound (then every value >= theta lies in that tile), else the whole grid.
+    bool loc0, loc1;
     {
       const float ob0 = __shfl_xor(best0, 32), ob1 = __shfl_xor(best1, 32);
       const int og0 = __shfl_xor(g0, 32), og1 = __shfl_xor(g1, 32);
       const bool oa0 = __shfl_xor((int)amb0, 32) != 0, oa1 = __shfl_xor((int)amb1, 32) != 0;
+      const float os0 = __shfl_xor(second0, 32), os1 = __shfl_xor(second1, 32);
+      const int obt = __shfl_xor(bt01, 32) ^ bt01;
       const bool tk0 = (ob0 > best0) | ((ob0 == best0) & (og0 < g0));
       const bool tk1 = (ob1 > best1) | ((ob1 == best1) & (og1 < g1));
       const float lo0 = tk0 ? best0 : ob0, lo1 = tk1 ? best1 : ob1;
@@ -695,17 +722,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       best1 = tk1 ? ob1 : best1;
       g1 = tk1 ? og1 : g1;
       amb1 = (tk1 ? oa1 : amb1) || lo1 >= best1 * (1.f - kAmbRel);
+      loc0 = (obt & 0xFFFF) == 0 && fmaxf(second0, os0) < best0 * (1.f - kAmbRel);
+      loc1 = (obt >> 16) == 0 && fmaxf(second1, os1) < best1 * (1.f - kAmbRel);
     }
     float best = h ? best1 : best0;  // own cell = column tile h
     int bidx = h ? g1 : g0;
     bool amb = h ? amb1 : amb0;
+    bool loc = h ? loc1 : loc0;
     if (bidx >= G) bidx = G - 1;
     float gval = best * (1.0f / kToepScale);
     // MUSIC: the reference's den > 1e-12 rule can only matter when the maximum is within rounding of M
-    if constexpr (MUSIC) amb = amb || best >= mthr;
+    if constexpr (MUSIC) {
+      const bool nearm = best >= mthr;  // the key rule may move the argmax anywhere: whole grid
+      amb = amb || nearm;
+      loc = loc && !nearm;
+    }
     // ambiguous: marked -1 - index for k_doa_fixup (the exact fp64 re-scan, launched right after this kernel; kept
     // out of this kernel so that its register allocation stays that of the scan loop)
-    if (amb) bidx = -1 - bidx;
+    if (amb) bidx = -1 - (bidx | (loc ? 0 : 1 << 24));
     pc = c < ncell ? (int)c : -1;
     pidx = bidx;
     pgv = gval;
@@ -716,15 +750,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   }
 }
 
-// Exact fp64 argmax of the cells k_doa_toep marked ambiguous (out_idx < 0: its f16 top-2 gap was inside kAmbRel, or a
-// MUSIC maximum within rounding of M): each wave reads 64 consecutive indices, and every marked cell is re-scanned by
-// the whole wave (coop_scan: lanes split the grid points).  One wave per 64 cells, all in parallel (a grid-stride
-// loop chained one index load per chunk: ~135 dependent round trips per wave at 2000 cfg2 frames).
-template <int MA, bool MUSIC>
+// Exact fp64 argmax of the cells a scan marked ambiguous (out_idx = -1 - (g | window << 24); k_doa_toep: its f16
+// top-2 gap inside kAmbRel, or a MUSIC maximum within rounding of M; k_doa_argmax / k_doa_scan: the f32 top-2 gap):
+// window 0 = the 32 grid points of g's tile (k_doa_toep, when every value within the bound lies in that tile), 1 =
+// the whole grid.  Each wave reads 64 consecutive indices and re-scans every marked cell with the whole wave
+// (coop_scan).  One wave per 64 cells, all in parallel (a grid-stride loop chained one index load per chunk).
+template <bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
                                                    const long long* __restrict__ ncell_dev, long long ncell_host, int G,
-                                                   const double* __restrict__ steer64, int* __restrict__ out_idx,
+                                                   const double2* __restrict__ steer64, int* __restrict__ out_idx,
                                                    float* __restrict__ out_gmax) {
   const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63;
@@ -737,15 +772,42 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
     while (fl) {
       const int src = __builtin_ctzll(fl);
       fl &= fl - 1;
+      const int code = -1 - __shfl(v, src);
+      const int g = code & 0xFFFFFF;
+      int lo = 0, hi = G;
+      if ((code >> 24) == 0) {
+        lo = g & ~31;
+        hi = lo + 32 < G ? lo + 32 : G;
+      }
       int xi;
       float xg;
-      coop_scan<MA, MUSIC>(rds, cfr, crc, ch * 64 + src, A, plane, fstride, G, steer64, xi, xg);
+      coop_scan<MUSIC>(rds, cfr, crc, ch * 64 + src, A, plane, fstride, lo, hi, steer64, xi, xg);
       if (lane == src) {
         out_idx[c] = xi;
         if (out_gmax) out_gmax[c] = xg;
       }
     }
   }
+}
+
+hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                            const int* c_rc, const long long* ncell_dev, long long ncell_host, int G, int music,
+                            const double* steer64, int* out_idx, float* out_gmax) {
+  if (A < 1 || A > 16 || G >= (1 << 24)) return hipErrorInvalidValue;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - code
+    if (atoi(e) == 1) return hipSuccess;
+#endif
+  long long fb = (ncell_host + 255) / 256;  // one wave per 64 cells
+  if (fb < 1) fb = 1;
+  const double2* s64 = reinterpret_cast<const double2*>(steer64);
+  if (music)
+    hipLaunchKernelGGL(k_doa_fixup<true>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
+                       ncell_dev, ncell_host, G, s64, out_idx, out_gmax);
+  else
+    hipLaunchKernelGGL(k_doa_fixup<false>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
+                       ncell_dev, ncell_host, G, s64, out_idx, out_gmax);
+  return hipGetLastError();
 }
 
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, bool SPEC = false>
@@ -795,16 +857,9 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
                      ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,
                      out_spec);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  // the exact re-scan of the marked cells: 256-thread blocks, one wave per 64 cells
-  long long fb = (ncell_host + 255) / 256;
-  if (fb < 1) fb = 1;
-#ifdef RSL_DEV_KNOBS
-  if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - index
-    if (atoi(e) == 1) return hipSuccess;
-#endif
-  hipLaunchKernelGGL((k_doa_fixup<MA, MUSIC>), dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
-                     ncell_dev, ncell_host, G, steer64, out_idx, out_gmax);
-  return hipGetLastError();
+  // the exact re-scan of the marked cells
+  return launch_doa_fixup(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, G, MUSIC, steer64, out_idx,
+                          out_gmax);
 }
 
 hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,

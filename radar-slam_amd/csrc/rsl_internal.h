@@ -61,6 +61,10 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
                            int ntiles, int G, int music, int* out_idx, float* out_gmax, float* out_spec,
                            long long spec_ld, int grid_blocks);
 // K5 fast path: Toeplitz-form argmax on f16 MFMA with hi/lo split (rsl_doa_toep.hip).
+// Exact fp64 re-scan of the cells a DoA scan marked ambiguous (out_idx < 0), rsl_doa_toep.hip k_doa_fixup.
+hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
+                            const int* c_rc, const long long* ncell_dev, long long ncell_host, int G, int music,
+                            const double* steer64, int* out_idx, float* out_gmax);
 hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
                            int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,

@@ -37,5 +37,7 @@ for nofix in ('0', '1', '0', '1'):
     ms = doa_ms()
     nc = int(ch.ncell_dev.item()) if hasattr(ch, 'ncell_dev') else -1
     g = ch.gidx[:nc].cpu().numpy() if nc > 0 else np.zeros(0)
-    print(f'nofix {nofix}: back half {ms:.3f} ms per {F} frames; cells {nc}; marked {(g < 0).sum()} '
-          f'({(g < 0).mean() * 100:.3f} %)', flush=True)
+    mk = g[g < 0]
+    full = int(((-1 - mk) >> 24).sum()) if mk.size else 0
+    print(f'nofix {nofix}: back half {ms:.3f} ms per {F} frames; cells {nc}; marked {mk.size} '
+          f'({(g < 0).mean() * 100:.3f} %), whole-grid re-scans {full}', flush=True)
