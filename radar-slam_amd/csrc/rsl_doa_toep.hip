@@ -630,6 +630,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         // the running SECOND joins the max tree (same 8 v_max3): m2 = max(second, tile max); since second <= best,
         // m2 > best <=> the tile max > best.  A record moves best to second; otherwise second = m2 (the largest tile
         // maximum of the other tiles: the end-of-pass ambiguity test)
+        if constexpr (DBG == 13) {  // timing ablation: no second tracking (the old record test, best folded in)
+          const float mb = tile_max(acc, best);
+          const bool r = mb > best;
+          best = mb;
+          if (r) {
+            set_bt(sh, t);
+            copy_tile(sv, acc);
+          }
+          return;
+        }
         // branch-free top-2: a record (m2 > best) leaves second = the old best, otherwise second = m2 -- both are
         // min(best, m2); best = max(best, m2).  Only the record tile's index and copy sit under the branch.
         // (integer min / max on the bit patterns, as in tile_max: the values are non-negative, and fminf / fmaxf
@@ -692,8 +702,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         const bool g0 = r0[i] >= th0, g1 = r1[i] >= th1;
         i0 = g0 ? i : i0;
         i1 = g1 ? i : i1;
-        two0 = two0 || (any0 && g0);
-        two1 = two1 || (any1 && g1);
+        if constexpr (DBG != 14) {  // DBG 14 (timing ablation): no count of the values >= theta
+          two0 = two0 || (any0 && g0);
+          two1 = two1 || (any1 && g1);
+        }
         any0 = any0 || g0;
         any1 = any1 || g1;
       }
@@ -833,6 +845,8 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 9) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 9, 12, true>;  // no tile loop
         if (v == 10) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 10, 12, true>;  // L2-resident signatures
         if (v == 11) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 11, 12, true>;  // prefetch 2 passes ahead
+        if (v == 13) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 13, 12, true>;  // no second tracking
+        if (v == 14) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 14, 12, true>;  // no in-tile count
       }
     }
   }
