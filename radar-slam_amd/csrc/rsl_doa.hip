@@ -55,14 +55,14 @@ RSL_DEV void load_sig(const float2* __restrict__ rds, const int* __restrict__ cf
 // Ambiguity bound of the f32 scans (relative top-2 gap): the [Re; Im] products are exact fp32 fmaf chains of <= 32
 // terms, so P = re^2 + im^2 is within a few fp32 ulps of the fp64 value of the same fp32 signature; a cell whose
 // best grid value is not this far above every other one (or, MUSIC, whose maximum is within rounding of M, where
-// the reference's den > 1e-12 rule may move the argmax) is marked -1 - (g | 1 << 24) and re-scanned over the whole
+// the reference's den > 1e-12 rule may move the argmax) is marked -1 (k_doa_fixup code 0) and re-scanned over the whole
 // grid in fp64 by k_doa_fixup (rsl_doa_toep.hip), so that no grid index differs from the fp64 argmax of the cell's
 // own signature by the scan's rounding.
 constexpr float kAmbRel32 = 4e-6f;
 
 RSL_DEV int mark_amb(int g, float best, float second, bool music, float Mf) {
   const bool amb = second >= best * (1.f - kAmbRel32) || !(best > 0.f) || (music && best >= Mf - 1e-4f);
-  return amb ? -1 - (g | (1 << 24)) : g;
+  return amb ? -1 : g;  // k_doa_fixup code 0: the whole grid
 }
 
 // One wave = 32 cells (two 16-column MFMA tiles) per pass over all grid tiles; the next pass's signature

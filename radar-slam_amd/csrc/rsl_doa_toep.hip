@@ -266,7 +266,7 @@ constexpr double kTieRel = 1e-12;
 template <bool MUSIC>
 RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
                        long long c, int A, size_t plane, size_t fstride, int g0, int g1,
-                       const double2* __restrict__ steer64, int& idx, float& gval) {
+                       const double2* __restrict__ steer64, int& idx, float& gval, double& kbest) {
   const int lane = threadIdx.x & 63;
   const int m = lane & 7, p = lane >> 3;
   const int fx = __builtin_amdgcn_readfirstlane(cfr[c]), fy = __builtin_amdgcn_readfirstlane(crc[c]);
@@ -328,6 +328,7 @@ RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ c
   }
   idx = bi;
   gval = (float)bp;
+  kbest = best;
 }
 
 // One wave = 64 cells per pass: lane (n, h) = (l & 31, l >> 5) loads, normalises and owns cell 64 ch + 32 h + n.
@@ -716,9 +717,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     int g1 = 32 * (bt01 >> 16) + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
     // merge the two K-half lanes of each column (first index wins on ties); ambiguous if the winner is, or if the
     // loser's maximum is within the bound of the winner's (an exact tie included)
-    // Window of the exact re-scan: the record tile alone when both K halves recorded in the same tile and no other
-    // tile of either half came within the bound (then every value >= theta lies in that tile), else the whole grid.
+    // Window of the exact re-scan: the record tiles of the two K halves when no other tile of either half came within
+    // the bound (then every value >= theta lies in those one or two tiles), else the whole grid.
     bool loc0, loc1;
+    int pbt;
     {
       const float ob0 = __shfl_xor(best0, 32), ob1 = __shfl_xor(best1, 32);
       const int og0 = __shfl_xor(g0, 32), og1 = __shfl_xor(g1, 32);
@@ -734,8 +736,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       best1 = tk1 ? ob1 : best1;
       g1 = tk1 ? og1 : g1;
       amb1 = (tk1 ? oa1 : amb1) || lo1 >= best1 * (1.f - kAmbRel);
-      loc0 = (obt & 0xFFFF) == 0 && fmaxf(second0, os0) < best0 * (1.f - kAmbRel);
-      loc1 = (obt >> 16) == 0 && fmaxf(second1, os1) < best1 * (1.f - kAmbRel);
+      loc0 = fmaxf(second0, os0) < best0 * (1.f - kAmbRel);
+      loc1 = fmaxf(second1, os1) < best1 * (1.f - kAmbRel);
+      pbt = obt ^ bt01;  // the partner K half's record tiles
     }
     float best = h ? best1 : best0;  // own cell = column tile h
     int bidx = h ? g1 : g0;
@@ -751,7 +754,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     }
     // ambiguous: marked -1 - index for k_doa_fixup (the exact fp64 re-scan, launched right after this kernel; kept
     // out of this kernel so that its register allocation stays that of the scan loop)
-    if (amb) bidx = -1 - (bidx | (loc ? 0 : 1 << 24));
+    if (amb) {
+      const int sh = h ? 16 : 0;
+      const int ta = (bt01 >> sh) & 0xFFFF, tb = (pbt >> sh) & 0xFFFF;
+      bidx = -1 - (loc ? (1 << 28) | (ta << 14) | tb : 0);  // k_doa_fixup's window code
+    }
     pc = c < ncell ? (int)c : -1;
     pidx = bidx;
     pgv = gval;
@@ -762,11 +769,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   }
 }
 
-// Exact fp64 argmax of the cells a scan marked ambiguous (out_idx = -1 - (g | window << 24); k_doa_toep: its f16
-// top-2 gap inside kAmbRel, or a MUSIC maximum within rounding of M; k_doa_argmax / k_doa_scan: the f32 top-2 gap):
-// window 0 = the 32 grid points of g's tile (k_doa_toep, when every value within the bound lies in that tile), 1 =
-// the whole grid.  Each wave reads 64 consecutive indices and re-scans every marked cell with the whole wave
-// (coop_scan).  One wave per 64 cells, all in parallel (a grid-stride loop chained one index load per chunk).
+// Exact fp64 argmax of the cells a scan marked ambiguous (out_idx = -1 - code; k_doa_toep: its f16 top-2 gap inside
+// kAmbRel, or a MUSIC maximum within rounding of M; k_doa_argmax / k_doa_scan: the f32 top-2 gap).  code bit 28 set:
+// re-scan the 32-point tiles (code >> 14) & 0x3FFF and code & 0x3FFF (the two K halves' record tiles, when every
+// value within the bound lies in them), else the whole grid.  A wave reads the indices of kFixChunks x 64 cells at
+// once and re-scans each marked cell with the whole wave (coop_scan).
+constexpr int kFixChunks = 8;
+
 template <bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
@@ -776,27 +785,49 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
   const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
-  const long long nch = (ncell + 63) >> 6;
-  for (long long ch = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); ch < nch; ch += (long long)gridDim.x * 4) {
-    const long long c = ch * 64 + lane;
-    const int v = c < ncell ? out_idx[c] : 0;
-    unsigned long long fl = __ballot(v < 0);
+  const long long c0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 * kFixChunks);
+  int v[kFixChunks];
+#pragma unroll
+  for (int k = 0; k < kFixChunks; ++k) {  // every index load in flight at once
+    const long long c = c0 + 64 * k + lane;
+    v[k] = c < ncell ? out_idx[c] : 0;
+  }
+#pragma unroll 1
+  for (int k = 0; k < kFixChunks; ++k) {
+    unsigned long long fl = __ballot(v[k] < 0);
     while (fl) {
       const int src = __builtin_ctzll(fl);
       fl &= fl - 1;
-      const int code = -1 - __shfl(v, src);
-      const int g = code & 0xFFFFFF;
-      int lo = 0, hi = G;
-      if ((code >> 24) == 0) {
-        lo = g & ~31;
-        hi = lo + 32 < G ? lo + 32 : G;
-      }
+      const int code = -1 - __shfl(v[k], src);
+      const long long cell = c0 + 64 * k + src;
       int xi;
       float xg;
-      coop_scan<MUSIC>(rds, cfr, crc, ch * 64 + src, A, plane, fstride, lo, hi, steer64, xi, xg);
+      double kx;
+      if ((code >> 28) & 1) {
+        int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
+        if (tb < ta) {
+          const int t = ta;
+          ta = tb;
+          tb = t;
+        }
+        coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 32 * ta, min(G, 32 * ta + 32), steer64, xi, xg, kx);
+        if (tb != ta) {  // the second tile: its (later) index must beat the tie tolerance
+          int yi;
+          float yg;
+          double ky;
+          coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 32 * tb, min(G, 32 * tb + 32), steer64, yi, yg,
+                           ky);
+          if (ky > kx + kTieRel * fabs(kx)) {
+            xi = yi;
+            xg = yg;
+          }
+        }
+      } else {
+        coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 0, G, steer64, xi, xg, kx);
+      }
       if (lane == src) {
-        out_idx[c] = xi;
-        if (out_gmax) out_gmax[c] = xg;
+        out_idx[cell] = xi;
+        if (out_gmax) out_gmax[cell] = xg;
       }
     }
   }
@@ -810,7 +841,7 @@ hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int
   if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - code
     if (atoi(e) == 1) return hipSuccess;
 #endif
-  long long fb = (ncell_host + 255) / 256;  // one wave per 64 cells
+  long long fb = (ncell_host + 256LL * kFixChunks - 1) / (256LL * kFixChunks);  // kFixChunks x 64 cells per wave
   if (fb < 1) fb = 1;
   const double2* s64 = reinterpret_cast<const double2*>(steer64);
   if (music)
