@@ -641,6 +641,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
           }
           return;
         }
+        if constexpr (DBG == 15) {  // variant: second = min(best, m2) (one op), best moved under the record branch
+          const float m2 = tile_max(acc, second);
+          const bool r = m2 > best;
+          second = __int_as_float(min(__float_as_int(best), __float_as_int(m2)));
+          if (r) {
+            best = m2;
+            set_bt(sh, t);
+            copy_tile(sv, acc);
+          }
+          return;
+        }
         // branch-free top-2: a record (m2 > best) leaves second = the old best, otherwise second = m2 -- both are
         // min(best, m2); best = max(best, m2).  Only the record tile's index and copy sit under the branch.
         // (integer min / max on the bit patterns, as in tile_max: the values are non-negative, and fminf / fmaxf
@@ -878,6 +889,7 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 11) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 11, 12, true>;  // prefetch 2 passes ahead
         if (v == 13) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 13, 12, true>;  // no second tracking
         if (v == 14) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 14, 12, true>;  // no in-tile count
+        if (v == 15) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 15, 12, true>;  // second by one min
       }
     }
   }
