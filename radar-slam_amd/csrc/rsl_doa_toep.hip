@@ -263,6 +263,23 @@ constexpr double kTieRel = 1e-12;
 // 16-B complex of a row, so a step's 64 lanes read 8 consecutive rows as contiguous 128-B runs (lanes splitting the
 // grid points with a whole row each read 16 lines per instruction: 16x the L2 requests); the sum over the antennas
 // is three xor shuffles inside the 8-lane group.  Returns (index, P at it) on every lane.
+// 64-bit DPP lane move (two 32-bit moves); CTRL is a DPP control with every lane of every row valid.
+template <int CTRL>
+RSL_DEV double dpp_d(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// Sum over each 8-lane group by DPP (quad_perm xor 1, xor 2, then row_half_mirror pairs the two quads): every lane
+// of the group gets the bit-identical sum, with no LDS round trip.
+RSL_DEV double sum8(double x) {
+  x += dpp_d<0xB1>(x);
+  x += dpp_d<0x4E>(x);
+  x += dpp_d<0x141>(x);
+  return x;
+}
+
 template <bool MUSIC>
 RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
                        long long c, int A, size_t plane, size_t fstride, int g0, int g1,
@@ -274,58 +291,52 @@ RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ c
   const float2 u0 = m < A ? base[(size_t)m * plane] : make_float2(0.f, 0.f);
   const float2 u1 = m + 8 < A ? base[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
   const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
-  double pw = x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1);
-  pw += __shfl_xor(pw, 1);
-  pw += __shfl_xor(pw, 2);
-  pw += __shfl_xor(pw, 4);
+  const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
   const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
   double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
   int bi = g1;
-  for (int gb = g0; gb < g1; gb += 8) {  // ascending g per 8-lane group: a later g must beat the tie tolerance
-    const int g = gb + p;
-    double zr = 0.0, zi = 0.0;
-    if (g < g1) {
-      const double2* row = steer64 + (size_t)g * A;
-      if (m < A) {
-        const double2 a = row[m];
-        zr = a.x * x0 + a.y * y0;  // conj(a) s
-        zi = a.x * y0 - a.y * x0;
-      }
-      if (m + 8 < A) {
-        const double2 a = row[m + 8];
-        zr += a.x * x1 + a.y * y1;
-        zi += a.x * y1 - a.y * x1;
+  for (int gb = g0; gb < g1; gb += 32) {  // 4 steps of 8 grid points, every steering load of the 4 issued first
+    double2 a0[4], a1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = gb + 8 * j + p;
+      a0[j] = make_double2(0.0, 0.0);
+      a1[j] = make_double2(0.0, 0.0);
+      if (g < g1) {
+        const double2* row = steer64 + (size_t)g * A;
+        if (m < A) a0[j] = row[m];
+        if (m + 8 < A) a1[j] = row[m + 8];
       }
     }
-    zr += __shfl_xor(zr, 1);
-    zi += __shfl_xor(zi, 1);
-    zr += __shfl_xor(zr, 2);
-    zi += __shfl_xor(zi, 2);
-    zr += __shfl_xor(zr, 4);
-    zi += __shfl_xor(zi, 4);
-    if (g < g1) {
-      const double pv = (zr * zr + zi * zi) * sc2;
-      const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
-      if (key > best + kTieRel * fabs(best)) {
-        best = key;
-        bi = g;
-        bp = pv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // ascending g per 8-lane group: a later g must beat the tie tolerance
+      const int g = gb + 8 * j + p;
+      const double zr = sum8(a0[j].x * x0 + a0[j].y * y0 + (a1[j].x * x1 + a1[j].y * y1));  // conj(a) s
+      const double zi = sum8(a0[j].x * y0 - a0[j].y * x0 + (a1[j].x * y1 - a1[j].y * x1));
+      if (g < g1) {
+        const double pv = (zr * zr + zi * zi) * sc2;
+        const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
+        if (key > best + kTieRel * fabs(best)) {
+          best = key;
+          bi = g;
+          bp = pv;
+        }
       }
     }
   }
-  // argmax over the 8 groups of (key, index): larger key beyond the tie tolerance, else lower index
-#pragma unroll
-  for (int off = 8; off < 64; off <<= 1) {
-    const double ok = __shfl_xor(best, off);
-    const int oi = __shfl_xor(bi, off);
-    const double op = __shfl_xor(bp, off);
+  // argmax over the 8 groups of (key, index): larger key beyond the tie tolerance, else lower index (xor 8 by DPP
+  // row_ror:8 inside each 16-lane row, then 16 and 32 by shuffles)
+  auto merge = [&](double ok, int oi, double op) {
     const double tol = kTieRel * fmax(fabs(ok), fabs(best));
     if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
       best = ok;
       bi = oi;
       bp = op;
     }
-  }
+  };
+  merge(dpp_d<0x128>(best), __builtin_amdgcn_update_dpp(0, bi, 0x128, 0xF, 0xF, false), dpp_d<0x128>(bp));
+#pragma unroll
+  for (int off = 16; off < 64; off <<= 1) merge(__shfl_xor(best, off), __shfl_xor(bi, off), __shfl_xor(bp, off));
   idx = bi;
   gval = (float)bp;
   kbest = best;
