@@ -242,7 +242,7 @@ RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
 }
 
 // Ambiguity bound of the f16 hi/lo scan, relative to a cell's maximum: a cell whose best grid value is not at least
-// this far above every other grid value (its top-2 gap) is re-scanned exactly in fp64 (coop_scan), so that the grid
+// this far above every other grid value (its top-2 gap) is re-scanned exactly in fp64 (k_doa_fixup), so that the grid
 // index is the fp64 argmax of the cell's own fp32 signature (no scan-caused flips).  The scan's
 // error is far smaller: the dropped T_lo r_lo term is <= 2^-22 sum |T_k| |r_k| and the fp32 autocorrelation and MFMA
 // accumulation add a few fp32 ulps of that sum (measured against the fp64 scan of the same signatures:
@@ -278,68 +278,6 @@ RSL_DEV double sum8(double x) {
   x += dpp_d<0x4E>(x);
   x += dpp_d<0x141>(x);
   return x;
-}
-
-template <bool MUSIC>
-RSL_DEV void coop_scan(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
-                       long long c, int A, size_t plane, size_t fstride, int g0, int g1,
-                       const double2* __restrict__ steer64, int& idx, float& gval, double& kbest) {
-  const int lane = threadIdx.x & 63;
-  const int m = lane & 7, p = lane >> 3;
-  const int fx = __builtin_amdgcn_readfirstlane(cfr[c]), fy = __builtin_amdgcn_readfirstlane(crc[c]);
-  const float2* base = rds + (size_t)fx * fstride + fy;
-  const float2 u0 = m < A ? base[(size_t)m * plane] : make_float2(0.f, 0.f);
-  const float2 u1 = m + 8 < A ? base[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
-  const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
-  const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
-  const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
-  double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
-  int bi = g1;
-  for (int gb = g0; gb < g1; gb += 32) {  // 4 steps of 8 grid points, every steering load of the 4 issued first
-    double2 a0[4], a1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int g = gb + 8 * j + p;
-      a0[j] = make_double2(0.0, 0.0);
-      a1[j] = make_double2(0.0, 0.0);
-      if (g < g1) {
-        const double2* row = steer64 + (size_t)g * A;
-        if (m < A) a0[j] = row[m];
-        if (m + 8 < A) a1[j] = row[m + 8];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // ascending g per 8-lane group: a later g must beat the tie tolerance
-      const int g = gb + 8 * j + p;
-      const double zr = sum8(a0[j].x * x0 + a0[j].y * y0 + (a1[j].x * x1 + a1[j].y * y1));  // conj(a) s
-      const double zi = sum8(a0[j].x * y0 - a0[j].y * x0 + (a1[j].x * y1 - a1[j].y * x1));
-      if (g < g1) {
-        const double pv = (zr * zr + zi * zi) * sc2;
-        const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
-        if (key > best + kTieRel * fabs(best)) {
-          best = key;
-          bi = g;
-          bp = pv;
-        }
-      }
-    }
-  }
-  // argmax over the 8 groups of (key, index): larger key beyond the tie tolerance, else lower index (xor 8 by DPP
-  // row_ror:8 inside each 16-lane row, then 16 and 32 by shuffles)
-  auto merge = [&](double ok, int oi, double op) {
-    const double tol = kTieRel * fmax(fabs(ok), fabs(best));
-    if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
-      best = ok;
-      bi = oi;
-      bp = op;
-    }
-  };
-  merge(dpp_d<0x128>(best), __builtin_amdgcn_update_dpp(0, bi, 0x128, 0xF, 0xF, false), dpp_d<0x128>(bp));
-#pragma unroll
-  for (int off = 16; off < 64; off <<= 1) merge(__shfl_xor(best, off), __shfl_xor(bi, off), __shfl_xor(bp, off));
-  idx = bi;
-  gval = (float)bp;
-  kbest = best;
 }
 
 // One wave = 64 cells per pass: lane (n, h) = (l & 31, l >> 5) loads, normalises and owns cell 64 ch + 32 h + n.
@@ -794,9 +732,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
 // Exact fp64 argmax of the cells a scan marked ambiguous (out_idx = -1 - code; k_doa_toep: its f16 top-2 gap inside
 // kAmbRel, or a MUSIC maximum within rounding of M; k_doa_argmax / k_doa_scan: the f32 top-2 gap).  code bit 28 set:
 // re-scan the 32-point tiles (code >> 14) & 0x3FFF and code & 0x3FFF (the two K halves' record tiles, when every
-// value within the bound lies in them), else the whole grid.  A wave reads the indices of kFixChunks x 64 cells at
-// once and re-scans each marked cell with the whole wave (coop_scan).
-constexpr int kFixChunks = 8;
+// value within the bound lies in them), else the whole grid.
+// Each wave reads the indices of kFixCells cells with coalesced 16-B loads, queues its marked cells in LDS, and
+// re-scans them 8 at a time, one cell per 8-lane group (lane = antenna m and m + 8, one grid point per step, the
+// steering loads of 4 steps issued together, the sum over antennas by DPP inside the group): the marked cells' memory
+// round trips overlap instead of running one cell after another through the whole wave.
+constexpr int kFixCells = 1024;
 
 template <bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
@@ -804,53 +745,110 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
                                                    const long long* __restrict__ ncell_dev, long long ncell_host, int G,
                                                    const double2* __restrict__ steer64, int* __restrict__ out_idx,
                                                    float* __restrict__ out_gmax) {
+  __shared__ int2 q[4][kFixCells];  // per wave: (cell - base, marked index) of its marked cells
+  __shared__ int qn[4];
   const long long ncell = list_count(ncell_dev, ncell_host);
-  const int lane = threadIdx.x & 63;
-  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
-  const long long c0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 * kFixChunks);
-  int v[kFixChunks];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long base = ((long long)blockIdx.x * 4 + wave) * kFixCells;
+  if (lane == 0) qn[wave] = 0;
+  __syncthreads();
+  const bool al = (reinterpret_cast<size_t>(out_idx) & 15) == 0;
+  int v[4][4];
 #pragma unroll
-  for (int k = 0; k < kFixChunks; ++k) {  // every index load in flight at once
-    const long long c = c0 + 64 * k + lane;
-    v[k] = c < ncell ? out_idx[c] : 0;
+  for (int j = 0; j < 4; ++j) {  // every index load in flight at once
+    const long long c0 = base + j * 256 + 4 * lane;
+    if (al && c0 + 3 < ncell) {
+      const int4 w = *reinterpret_cast<const int4*>(out_idx + c0);
+      v[j][0] = w.x;
+      v[j][1] = w.y;
+      v[j][2] = w.z;
+      v[j][3] = w.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[j][k] = c0 + k < ncell ? out_idx[c0 + k] : 0;
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (v[j][k] < 0) {
+        const int pos = atomicAdd(&qn[wave], 1);
+        q[wave][pos] = make_int2(j * 256 + 4 * lane + k, v[j][k]);
+      }
+  __syncthreads();
+  const int n = qn[wave];
+  const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
+  const int m = lane & 7;
+  for (int q0 = 0; q0 < n; q0 += 8) {
+    const int jq = q0 + (lane >> 3);
+    const bool act = jq < n;
+    const int2 e = act ? q[wave][jq] : make_int2(0, -1);
+    const long long cell = base + e.x;
+    const int code = -1 - e.y;
+    // window: one or two 32-point tiles (ascending), or the whole grid
+    int lo0 = 0, hi0 = G, lo1 = 0, hi1 = 0;
+    if ((code >> 28) & 1) {
+      int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
+      if (tb < ta) {
+        const int t = ta;
+        ta = tb;
+        tb = t;
+      }
+      lo0 = 32 * ta;
+      hi0 = min(G, lo0 + 32);
+      if (tb != ta) {
+        lo1 = 32 * tb;
+        hi1 = min(G, lo1 + 32);
+      }
+    }
+    if (!act) hi0 = 0;
+    float2 u0 = make_float2(0.f, 0.f), u1 = make_float2(0.f, 0.f);
+    if (act) {
+      const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
+      if (m < A) u0 = sb[(size_t)m * plane];
+      if (m + 8 < A) u1 = sb[(size_t)(m + 8) * plane];
+    }
+    const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
+    const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
+    const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
+    double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
+    int bi = G;
 #pragma unroll 1
-  for (int k = 0; k < kFixChunks; ++k) {
-    unsigned long long fl = __ballot(v[k] < 0);
-    while (fl) {
-      const int src = __builtin_ctzll(fl);
-      fl &= fl - 1;
-      const int code = -1 - __shfl(v[k], src);
-      const long long cell = c0 + 64 * k + src;
-      int xi;
-      float xg;
-      double kx;
-      if ((code >> 28) & 1) {
-        int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
-        if (tb < ta) {
-          const int t = ta;
-          ta = tb;
-          tb = t;
-        }
-        coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 32 * ta, min(G, 32 * ta + 32), steer64, xi, xg, kx);
-        if (tb != ta) {  // the second tile: its (later) index must beat the tie tolerance
-          int yi;
-          float yg;
-          double ky;
-          coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 32 * tb, min(G, 32 * tb + 32), steer64, yi, yg,
-                           ky);
-          if (ky > kx + kTieRel * fabs(kx)) {
-            xi = yi;
-            xg = yg;
+    for (int seg = 0; seg < 2; ++seg) {
+      const int lo = seg ? lo1 : lo0, hi = seg ? hi1 : hi0;
+#pragma unroll 1
+      for (int gb = lo; gb < hi; gb += 4) {  // ascending g: a later g must beat the tie tolerance
+        double2 a0[4], a1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          a0[k] = make_double2(0.0, 0.0);
+          a1[k] = make_double2(0.0, 0.0);
+          if (gb + k < hi) {
+            const double2* row = steer64 + (size_t)(gb + k) * A;
+            if (m < A) a0[k] = row[m];
+            if (m + 8 < A) a1[k] = row[m + 8];
           }
         }
-      } else {
-        coop_scan<MUSIC>(rds, cfr, crc, cell, A, plane, fstride, 0, G, steer64, xi, xg, kx);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double zr = sum8(a0[k].x * x0 + a0[k].y * y0 + (a1[k].x * x1 + a1[k].y * y1));  // conj(a) s
+          const double zi = sum8(a0[k].x * y0 - a0[k].y * x0 + (a1[k].x * y1 - a1[k].y * x1));
+          if (gb + k < hi) {
+            const double pv = (zr * zr + zi * zi) * sc2;
+            const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
+            if (key > best + kTieRel * fabs(best)) {
+              best = key;
+              bi = gb + k;
+              bp = pv;
+            }
+          }
+        }
       }
-      if (lane == src) {
-        out_idx[cell] = xi;
-        if (out_gmax) out_gmax[cell] = xg;
-      }
+    }
+    if (act && m == 0) {
+      out_idx[cell] = bi;
+      if (out_gmax) out_gmax[cell] = (float)bp;
     }
   }
 }
@@ -863,7 +861,7 @@ hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int
   if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - code
     if (atoi(e) == 1) return hipSuccess;
 #endif
-  long long fb = (ncell_host + 256LL * kFixChunks - 1) / (256LL * kFixChunks);  // kFixChunks x 64 cells per wave
+  long long fb = (ncell_host + 4LL * kFixCells - 1) / (4LL * kFixCells);  // kFixCells cells per wave
   if (fb < 1) fb = 1;
   const double2* s64 = reinterpret_cast<const double2*>(steer64);
   if (music)

@@ -38,6 +38,6 @@ for nofix in ('0', '1', '0', '1'):
     nc = int(ch.ncell_dev.item()) if hasattr(ch, 'ncell_dev') else -1
     g = ch.gidx[:nc].cpu().numpy() if nc > 0 else np.zeros(0)
     mk = g[g < 0]
-    full = int(((-1 - mk) >> 24).sum()) if mk.size else 0
+    full = int(((((-1 - mk) >> 28) & 1) == 0).sum()) if mk.size else 0
     print(f'nofix {nofix}: back half {ms:.3f} ms per {F} frames; cells {nc}; marked {mk.size} '
           f'({(g < 0).mean() * 100:.3f} %), whole-grid re-scans {full}', flush=True)
