@@ -735,7 +735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
 // value within the bound lies in them), else the whole grid.
 // Each wave reads the indices of kFixCells cells with coalesced 16-B loads, queues its marked cells in LDS, and
 // re-scans them 8 at a time, one cell per 8-lane group (lane = antenna m and m + 8, one grid point per step, the
-// steering loads of 4 steps issued together, the sum over antennas by DPP inside the group): the marked cells' memory
+// steering loads of 8 steps issued together, the sum over antennas by DPP inside the group): the marked cells' memory
 // round trips overlap instead of running one cell after another through the whole wave.
 constexpr int kFixCells = 1024;
 
@@ -746,11 +746,14 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
                                                    const double2* __restrict__ steer64, int* __restrict__ out_idx,
                                                    float* __restrict__ out_gmax) {
   __shared__ int2 q[4][kFixCells];  // per wave: (cell - base, marked index) of its marked cells
-  __shared__ int qn[4];
+  __shared__ int qn[4], qf[4];
   const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long base = ((long long)blockIdx.x * 4 + wave) * kFixCells;
-  if (lane == 0) qn[wave] = 0;
+  if (lane == 0) {
+    qn[wave] = 0;
+    qf[wave] = 0;
+  }
   __syncthreads();
   const bool al = (reinterpret_cast<size_t>(out_idx) & 15) == 0;
   int v[4][4];
@@ -772,12 +775,13 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (v[j][k] < 0) {
-        const int pos = atomicAdd(&qn[wave], 1);
+      if (v[j][k] < 0) {  // windowed cells from the front of the queue, whole-grid cells from the back
+        const bool win = ((-1 - v[j][k]) >> 28) & 1;
+        const int pos = win ? atomicAdd(&qn[wave], 1) : kFixCells - 1 - atomicAdd(&qf[wave], 1);
         q[wave][pos] = make_int2(j * 256 + 4 * lane + k, v[j][k]);
       }
   __syncthreads();
-  const int n = qn[wave];
+  const int n = qn[wave], nf = qf[wave];
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
   const int m = lane & 7;
   for (int q0 = 0; q0 < n; q0 += 8) {
@@ -786,9 +790,9 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
     const int2 e = act ? q[wave][jq] : make_int2(0, -1);
     const long long cell = base + e.x;
     const int code = -1 - e.y;
-    // window: one or two 32-point tiles (ascending), or the whole grid
-    int lo0 = 0, hi0 = G, lo1 = 0, hi1 = 0;
-    if ((code >> 28) & 1) {
+    // window: one or two 32-point tiles (ascending)
+    int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+    {
       int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
       if (tb < ta) {
         const int t = ta;
@@ -818,10 +822,10 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
     for (int seg = 0; seg < 2; ++seg) {
       const int lo = seg ? lo1 : lo0, hi = seg ? hi1 : hi0;
 #pragma unroll 1
-      for (int gb = lo; gb < hi; gb += 4) {  // ascending g: a later g must beat the tie tolerance
-        double2 a0[4], a1[4];
+      for (int gb = lo; gb < hi; gb += 8) {  // ascending g: a later g must beat the tie tolerance
+        double2 a0[8], a1[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
           a0[k] = make_double2(0.0, 0.0);
           a1[k] = make_double2(0.0, 0.0);
           if (gb + k < hi) {
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
           }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
           const double zr = sum8(a0[k].x * x0 + a0[k].y * y0 + (a1[k].x * x1 + a1[k].y * y1));  // conj(a) s
           const double zi = sum8(a0[k].x * y0 - a0[k].y * x0 + (a1[k].x * y1 - a1[k].y * x1));
           if (gb + k < hi) {
@@ -847,6 +851,69 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
       }
     }
     if (act && m == 0) {
+      out_idx[cell] = bi;
+      if (out_gmax) out_gmax[cell] = (float)bp;
+    }
+  }
+  // whole-grid cells: one at a time by the whole wave (group p = lane >> 3 takes grid points g = 64 i + 8 j + p,
+  // j < 8, every steering load of the 8 steps issued together), then the argmax over the groups
+  const int p = lane >> 3;
+#pragma unroll 1
+  for (int f = 0; f < nf; ++f) {
+    const int2 e = q[wave][kFixCells - 1 - f];
+    const long long cell = base + e.x;
+    const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
+    const float2 u0 = m < A ? sb[(size_t)m * plane] : make_float2(0.f, 0.f);
+    const float2 u1 = m + 8 < A ? sb[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
+    const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
+    const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
+    const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;
+    double best = -2.0, bp = 0.0;
+    int bi = G;
+#pragma unroll 1
+    for (int gb = 0; gb < G; gb += 64) {
+      double2 a0[8], a1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int g = gb + 8 * j + p;
+        a0[j] = make_double2(0.0, 0.0);
+        a1[j] = make_double2(0.0, 0.0);
+        if (g < G) {
+          const double2* row = steer64 + (size_t)g * A;
+          if (m < A) a0[j] = row[m];
+          if (m + 8 < A) a1[j] = row[m + 8];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // ascending g per group
+        const int g = gb + 8 * j + p;
+        const double zr = sum8(a0[j].x * x0 + a0[j].y * y0 + (a1[j].x * x1 + a1[j].y * y1));
+        const double zi = sum8(a0[j].x * y0 - a0[j].y * x0 + (a1[j].x * y1 - a1[j].y * x1));
+        if (g < G) {
+          const double pv = (zr * zr + zi * zi) * sc2;
+          const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
+          if (key > best + kTieRel * fabs(best)) {
+            best = key;
+            bi = g;
+            bp = pv;
+          }
+        }
+      }
+    }
+    // argmax over the 8 groups: larger key beyond the tie tolerance, else lower index (xor 8 by DPP row_ror:8
+    // inside each 16-lane row, then 16 and 32 by shuffles)
+    auto merge = [&](double ok, int oi, double op) {
+      const double tol = kTieRel * fmax(fabs(ok), fabs(best));
+      if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
+        best = ok;
+        bi = oi;
+        bp = op;
+      }
+    };
+    merge(dpp_d<0x128>(best), __builtin_amdgcn_update_dpp(0, bi, 0x128, 0xF, 0xF, false), dpp_d<0x128>(bp));
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) merge(__shfl_xor(best, off), __shfl_xor(bi, off), __shfl_xor(bp, off));
+    if (lane == 0) {
       out_idx[cell] = bi;
       if (out_gmax) out_gmax[cell] = (float)bp;
     }
