@@ -263,23 +263,6 @@ constexpr double kTieRel = 1e-12;
 // 16-B complex of a row, so a step's 64 lanes read 8 consecutive rows as contiguous 128-B runs (lanes splitting the
 // grid points with a whole row each read 16 lines per instruction: 16x the L2 requests); the sum over the antennas
 // is three xor shuffles inside the 8-lane group.  Returns (index, P at it) on every lane.
-// 64-bit DPP lane move (two 32-bit moves); CTRL is a DPP control with every lane of every row valid.
-template <int CTRL>
-RSL_DEV double dpp_d(double x) {
-  const long long v = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// Sum over each 8-lane group by DPP (quad_perm xor 1, xor 2, then row_half_mirror pairs the two quads): every lane
-// of the group gets the bit-identical sum, with no LDS round trip.
-RSL_DEV double sum8(double x) {
-  x += dpp_d<0xB1>(x);
-  x += dpp_d<0x4E>(x);
-  x += dpp_d<0x141>(x);
-  return x;
-}
-
 // One wave = 64 cells per pass: lane (n, h) = (l & 31, l >> 5) loads, normalises and owns cell 64 ch + 32 h + n.
 // The two 32-cell halves are the two column tiles of v_mfma_f32_32x32x16_f16 (B: lane holds K rows 8h..8h+7 of
 // column n), so each lane computes the Toeplitz column of its own cell once and swaps the other K half with
@@ -733,163 +716,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
 // kAmbRel, or a MUSIC maximum within rounding of M; k_doa_argmax / k_doa_scan: the f32 top-2 gap).  code bit 28 set:
 // re-scan the 32-point tiles (code >> 14) & 0x3FFF and code & 0x3FFF (the two K halves' record tiles, when every
 // value within the bound lies in them), else the whole grid.
-// Each wave reads the indices of kFixCells cells with coalesced 16-B loads, queues its marked cells in LDS, and
-// re-scans them 8 at a time, one cell per 8-lane group (lane = antenna m and m + 8, one grid point per step, the
-// steering loads of 8 steps issued together, the sum over antennas by DPP inside the group): the marked cells' memory
-// round trips overlap instead of running one cell after another through the whole wave.
-constexpr int kFixCells = 1024;
+// A wave reads the indices of kFixCells cells (coalesced 16-B loads, 256 cells per step) and queues its marked
+// cells in LDS; 8 queued cells at a time, the lanes (cell, antenna) load the cells' signatures into LDS together (one
+// memory round trip for 8 cells), then each cell is re-scanned by the whole wave with one grid point per lane
+// (lanes 0-31 / 32-63 = the two window tiles, or 64 grid points per pass over the whole grid) from the transposed
+// fp64 table steerT[m][g] (a lane's antenna loads are 16 B of consecutive grid points: each load instruction reads
+// one or two contiguous runs), and a wave argmax with the tie rule.
+constexpr int kFixCells = 2048;
+constexpr int kFixQ = 256 + 8;  // queue entries per wave: a step adds at most 256
 
 template <bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
                                                    const long long* __restrict__ ncell_dev, long long ncell_host, int G,
-                                                   const double2* __restrict__ steer64, int* __restrict__ out_idx,
+                                                   const double2* __restrict__ steerT, int* __restrict__ out_idx,
                                                    float* __restrict__ out_gmax) {
-  __shared__ int2 q[4][kFixCells];  // per wave: (cell - base, marked index) of its marked cells
-  __shared__ int qn[4], qf[4];
+  __shared__ int2 q[4][kFixQ];        // (cell - base, marked index)
+  __shared__ float2 sig[4][8][16];    // the signatures of the 8 cells being re-scanned
+  __shared__ int qn[4];
   const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long base = ((long long)blockIdx.x * 4 + wave) * kFixCells;
-  if (lane == 0) {
-    qn[wave] = 0;
-    qf[wave] = 0;
-  }
-  __syncthreads();
-  const bool al = (reinterpret_cast<size_t>(out_idx) & 15) == 0;
-  int v[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {  // every index load in flight at once
-    const long long c0 = base + j * 256 + 4 * lane;
-    if (al && c0 + 3 < ncell) {
-      const int4 w = *reinterpret_cast<const int4*>(out_idx + c0);
-      v[j][0] = w.x;
-      v[j][1] = w.y;
-      v[j][2] = w.z;
-      v[j][3] = w.w;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[j][k] = c0 + k < ncell ? out_idx[c0 + k] : 0;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (v[j][k] < 0) {  // windowed cells from the front of the queue, whole-grid cells from the back
-        const bool win = ((-1 - v[j][k]) >> 28) & 1;
-        const int pos = win ? atomicAdd(&qn[wave], 1) : kFixCells - 1 - atomicAdd(&qf[wave], 1);
-        q[wave][pos] = make_int2(j * 256 + 4 * lane + k, v[j][k]);
-      }
-  __syncthreads();
-  const int n = qn[wave], nf = qf[wave];
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
-  const int m = lane & 7;
-  for (int q0 = 0; q0 < n; q0 += 8) {
-    const int jq = q0 + (lane >> 3);
-    const bool act = jq < n;
-    const int2 e = act ? q[wave][jq] : make_int2(0, -1);
-    const long long cell = base + e.x;
-    const int code = -1 - e.y;
-    // window: one or two 32-point tiles (ascending)
-    int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
-    {
-      int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
-      if (tb < ta) {
-        const int t = ta;
-        ta = tb;
-        tb = t;
-      }
-      lo0 = 32 * ta;
-      hi0 = min(G, lo0 + 32);
-      if (tb != ta) {
-        lo1 = 32 * tb;
-        hi1 = min(G, lo1 + 32);
-      }
-    }
-    if (!act) hi0 = 0;
-    float2 u0 = make_float2(0.f, 0.f), u1 = make_float2(0.f, 0.f);
-    if (act) {
-      const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
-      if (m < A) u0 = sb[(size_t)m * plane];
-      if (m + 8 < A) u1 = sb[(size_t)(m + 8) * plane];
-    }
-    const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
-    const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
-    const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
-    double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
-    int bi = G;
-#pragma unroll 1
-    for (int seg = 0; seg < 2; ++seg) {
-      const int lo = seg ? lo1 : lo0, hi = seg ? hi1 : hi0;
-#pragma unroll 1
-      for (int gb = lo; gb < hi; gb += 8) {  // ascending g: a later g must beat the tie tolerance
-        double2 a0[8], a1[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          a0[k] = make_double2(0.0, 0.0);
-          a1[k] = make_double2(0.0, 0.0);
-          if (gb + k < hi) {
-            const double2* row = steer64 + (size_t)(gb + k) * A;
-            if (m < A) a0[k] = row[m];
-            if (m + 8 < A) a1[k] = row[m + 8];
-          }
+  const bool al = (reinterpret_cast<size_t>(out_idx) & 15) == 0;
+  auto lds_sync = [] {  // this wave's LDS writes visible to its own later LDS reads
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (lane == 0) qn[wave] = 0;
+  lds_sync();
+  auto rescan = [&](int n) {  // the queued cells, 8 per round
+    for (int e0 = 0; e0 < n; e0 += 8) {
+      {  // signatures of up to 8 cells: lane (e, m) loads antennas m and m + 8 of cell e0 + e
+        const int e = e0 + (lane >> 3), m = lane & 7;
+        if (e < n) {
+          const long long cell = base + q[wave][e].x;
+          const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
+          sig[wave][lane >> 3][m] = m < A ? sb[(size_t)m * plane] : make_float2(0.f, 0.f);
+          sig[wave][lane >> 3][m + 8] = m + 8 < A ? sb[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
         }
+      }
+      lds_sync();
+      const int ne = min(8, n - e0);
+      for (int e = 0; e < ne; ++e) {  // wave-uniform
+        const int2 en = q[wave][e0 + e];
+        const long long cell = base + en.x;
+        const int code = -1 - en.y;
+        double sr[16], si[16], pw = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const double zr = sum8(a0[k].x * x0 + a0[k].y * y0 + (a1[k].x * x1 + a1[k].y * y1));  // conj(a) s
-          const double zi = sum8(a0[k].x * y0 - a0[k].y * x0 + (a1[k].x * y1 - a1[k].y * x1));
-          if (gb + k < hi) {
-            const double pv = (zr * zr + zi * zi) * sc2;
-            const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
-            if (key > best + kTieRel * fabs(best)) {
-              best = key;
-              bi = gb + k;
-              bp = pv;
+        for (int m = 0; m < 16; ++m) {
+          const float2 z = sig[wave][e][m];
+          sr[m] = z.x;
+          si[m] = z.y;
+          pw += sr[m] * sr[m] + si[m] * si[m];
+        }
+        const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;  // unit-norm signature (angle_estimation.py:86-88)
+        double best = -2.0, bp = 0.0;  // below every key (keys are P >= 0 or -1)
+        int bi = G;
+        auto point = [&](int g) {  // ascending g per lane: a later g must beat the tie tolerance
+          double zr = 0.0, zi = 0.0;
+#pragma unroll
+          for (int m = 0; m < 16; ++m)
+            if (m < A) {
+              const double2 a = steerT[(size_t)m * G + g];
+              zr += a.x * sr[m] + a.y * si[m];  // conj(a) s
+              zi += a.x * si[m] - a.y * sr[m];
             }
-          }
-        }
-      }
-    }
-    if (act && m == 0) {
-      out_idx[cell] = bi;
-      if (out_gmax) out_gmax[cell] = (float)bp;
-    }
-  }
-  // whole-grid cells: one at a time by the whole wave (group p = lane >> 3 takes grid points g = 64 i + 8 j + p,
-  // j < 8, every steering load of the 8 steps issued together), then the argmax over the groups
-  const int p = lane >> 3;
-#pragma unroll 1
-  for (int f = 0; f < nf; ++f) {
-    const int2 e = q[wave][kFixCells - 1 - f];
-    const long long cell = base + e.x;
-    const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
-    const float2 u0 = m < A ? sb[(size_t)m * plane] : make_float2(0.f, 0.f);
-    const float2 u1 = m + 8 < A ? sb[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
-    const double x0 = u0.x, y0 = u0.y, x1 = u1.x, y1 = u1.y;
-    const double pw = sum8(x0 * x0 + y0 * y0 + (x1 * x1 + y1 * y1));
-    const double sc2 = pw > 0.0 ? 1.0 / pw : 1.0;
-    double best = -2.0, bp = 0.0;
-    int bi = G;
-#pragma unroll 1
-    for (int gb = 0; gb < G; gb += 64) {
-      double2 a0[8], a1[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int g = gb + 8 * j + p;
-        a0[j] = make_double2(0.0, 0.0);
-        a1[j] = make_double2(0.0, 0.0);
-        if (g < G) {
-          const double2* row = steer64 + (size_t)g * A;
-          if (m < A) a0[j] = row[m];
-          if (m + 8 < A) a1[j] = row[m + 8];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {  // ascending g per group
-        const int g = gb + 8 * j + p;
-        const double zr = sum8(a0[j].x * x0 + a0[j].y * y0 + (a1[j].x * x1 + a1[j].y * y1));
-        const double zi = sum8(a0[j].x * y0 - a0[j].y * x0 + (a1[j].x * y1 - a1[j].y * x1));
-        if (g < G) {
           const double pv = (zr * zr + zi * zi) * sc2;
           const double key = MUSIC ? (((double)A - pv > 1e-12) ? pv : -1.0) : pv;
           if (key > best + kTieRel * fabs(best)) {
@@ -897,26 +789,74 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
             bi = g;
             bp = pv;
           }
+        };
+        if ((code >> 28) & 1) {
+          int ta = (code >> 14) & 0x3FFF, tb = code & 0x3FFF;
+          if (tb < ta) {
+            const int t = ta;
+            ta = tb;
+            tb = t;
+          }
+          const int t = lane < 32 ? ta : tb;
+          const int g = 32 * t + (lane & 31);
+          if (g < G && (lane < 32 || tb != ta)) point(g);
+        } else {
+#pragma unroll 1
+          for (int g = lane; g < G; g += 64) point(g);
+        }
+        // wave argmax: larger key beyond the tie tolerance, else lower index
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const double ok = __shfl_xor(best, off), op = __shfl_xor(bp, off);
+          const int oi = __shfl_xor(bi, off);
+          const double tol = kTieRel * fmax(fabs(ok), fabs(best));
+          if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
+            best = ok;
+            bi = oi;
+            bp = op;
+          }
+        }
+        if (lane == 0) {
+          out_idx[cell] = bi;
+          if (out_gmax) out_gmax[cell] = (float)bp;
         }
       }
+      lds_sync();  // the next round overwrites sig
     }
-    // argmax over the 8 groups: larger key beyond the tie tolerance, else lower index (xor 8 by DPP row_ror:8
-    // inside each 16-lane row, then 16 and 32 by shuffles)
-    auto merge = [&](double ok, int oi, double op) {
-      const double tol = kTieRel * fmax(fabs(ok), fabs(best));
-      if (ok > best + tol || (fabs(ok - best) <= tol && oi < bi)) {
-        best = ok;
-        bi = oi;
-        bp = op;
-      }
-    };
-    merge(dpp_d<0x128>(best), __builtin_amdgcn_update_dpp(0, bi, 0x128, 0xF, 0xF, false), dpp_d<0x128>(bp));
+  };
+#pragma unroll 1
+  for (int st = 0; st < kFixCells; st += 256) {
+    const long long c0 = base + st + 4 * lane;
+    int v[4];
+    if (al && c0 + 3 < ncell) {
+      const int4 w = *reinterpret_cast<const int4*>(out_idx + c0);
+      v[0] = w.x;
+      v[1] = w.y;
+      v[2] = w.z;
+      v[3] = w.w;
+    } else {
 #pragma unroll
-    for (int off = 16; off < 64; off <<= 1) merge(__shfl_xor(best, off), __shfl_xor(bi, off), __shfl_xor(bp, off));
-    if (lane == 0) {
-      out_idx[cell] = bi;
-      if (out_gmax) out_gmax[cell] = (float)bp;
+      for (int k = 0; k < 4; ++k) v[k] = c0 + k < ncell ? out_idx[c0 + k] : 0;
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (v[k] < 0) q[wave][atomicAdd(&qn[wave], 1)] = make_int2(st + 4 * lane + k, v[k]);
+    lds_sync();
+    const int n = qn[wave];
+    if (n >= 8 || st + 256 >= kFixCells) {  // full rounds now; the remainder after the last step
+      rescan(n);
+      if (lane == 0) qn[wave] = 0;
+      lds_sync();
+    }
+  }
+}
+
+// steerT[m][g] = steer64[g][m] (fp64 complex), the fixup's coalesced layout
+__global__ void k_steer_transpose(const double2* __restrict__ steer64, int G, int A, double2* __restrict__ steerT) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < G * A) {
+    const int g = x / A, m = x - g * A;
+    steerT[(size_t)m * G + g] = steer64[x];
   }
 }
 
@@ -930,14 +870,21 @@ hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int
 #endif
   long long fb = (ncell_host + 4LL * kFixCells - 1) / (4LL * kFixCells);  // kFixCells cells per wave
   if (fb < 1) fb = 1;
-  const double2* s64 = reinterpret_cast<const double2*>(steer64);
+  // the transposed table lives for this call only (stream-ordered allocation: concurrent calls on other streams with
+  // other steering tables cannot race on it)
+  double2* tT = nullptr;
+  if (hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tT), sizeof(double2) * (size_t)G * A, st)) return e;
+  hipLaunchKernelGGL(k_steer_transpose, dim3((unsigned)((G * A + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const double2*>(steer64), G, A, tT);
   if (music)
     hipLaunchKernelGGL(k_doa_fixup<true>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
-                       ncell_dev, ncell_host, G, s64, out_idx, out_gmax);
+                       ncell_dev, ncell_host, G, tT, out_idx, out_gmax);
   else
     hipLaunchKernelGGL(k_doa_fixup<false>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
-                       ncell_dev, ncell_host, G, s64, out_idx, out_gmax);
-  return hipGetLastError();
+                       ncell_dev, ncell_host, G, tT, out_idx, out_gmax);
+  const hipError_t e = hipGetLastError();
+  const hipError_t f = hipFreeAsync(tT, st);
+  return e != hipSuccess ? e : f;
 }
 
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, bool SPEC = false>
