@@ -725,14 +725,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
 constexpr int kFixCells = 2048;
 constexpr int kFixQ = 256 + 8;  // queue entries per wave: a step adds at most 256
 
-template <bool MUSIC>
+template <int MA, bool MUSIC>
 __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rds, int A, int S, int C,
                                                    const int* __restrict__ cfr, const int* __restrict__ crc,
                                                    const long long* __restrict__ ncell_dev, long long ncell_host, int G,
                                                    const double2* __restrict__ steerT, int* __restrict__ out_idx,
                                                    float* __restrict__ out_gmax) {
   __shared__ int2 q[4][kFixQ];        // (cell - base, marked index)
-  __shared__ float2 sig[4][8][16];    // the signatures of the 8 cells being re-scanned
+  __shared__ float2 sig[4][8][MA];    // the signatures of the 8 cells being re-scanned
   __shared__ int qn[4];
   const long long ncell = list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
           const long long cell = base + q[wave][e].x;
           const float2* sb = rds + (size_t)cfr[cell] * fstride + crc[cell];
           sig[wave][lane >> 3][m] = m < A ? sb[(size_t)m * plane] : make_float2(0.f, 0.f);
-          sig[wave][lane >> 3][m + 8] = m + 8 < A ? sb[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
+          if constexpr (MA > 8) sig[wave][lane >> 3][m + 8] = m + 8 < A ? sb[(size_t)(m + 8) * plane] : make_float2(0.f, 0.f);
         }
       }
       lds_sync();
@@ -762,9 +762,9 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
         const int2 en = q[wave][e0 + e];
         const long long cell = base + en.x;
         const int code = -1 - en.y;
-        double sr[16], si[16], pw = 0.0;
+        double sr[MA], si[MA], pw = 0.0;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
+        for (int m = 0; m < MA; ++m) {
           const float2 z = sig[wave][e][m];
           sr[m] = z.x;
           si[m] = z.y;
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
         auto point = [&](int g) {  // ascending g per lane: a later g must beat the tie tolerance
           double zr = 0.0, zi = 0.0;
 #pragma unroll
-          for (int m = 0; m < 16; ++m)
+          for (int m = 0; m < MA; ++m)
             if (m < A) {
               const double2 a = steerT[(size_t)m * G + g];
               zr += a.x * sr[m] + a.y * si[m];  // conj(a) s
@@ -824,20 +824,24 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
       lds_sync();  // the next round overwrites sig
     }
   };
-#pragma unroll 1
-  for (int st = 0; st < kFixCells; st += 256) {
-    const long long c0 = base + st + 4 * lane;
-    int v[4];
-    if (al && c0 + 3 < ncell) {
-      const int4 w = *reinterpret_cast<const int4*>(out_idx + c0);
-      v[0] = w.x;
-      v[1] = w.y;
-      v[2] = w.z;
-      v[3] = w.w;
-    } else {
+  constexpr int NST = kFixCells / 256;
+  int4 vv[NST];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = c0 + k < ncell ? out_idx[c0 + k] : 0;
+  for (int j = 0; j < NST; ++j) {  // every index load in flight at once
+    const long long c0 = base + j * 256 + 4 * lane;
+    if (al && c0 + 3 < ncell) {
+      vv[j] = *reinterpret_cast<const int4*>(out_idx + c0);
+    } else {
+      vv[j].x = c0 < ncell ? out_idx[c0] : 0;
+      vv[j].y = c0 + 1 < ncell ? out_idx[c0 + 1] : 0;
+      vv[j].z = c0 + 2 < ncell ? out_idx[c0 + 2] : 0;
+      vv[j].w = c0 + 3 < ncell ? out_idx[c0 + 3] : 0;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < NST; ++j) {
+    const int st = j * 256;
+    const int v[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (v[k] < 0) q[wave][atomicAdd(&qn[wave], 1)] = make_int2(st + 4 * lane + k, v[k]);
@@ -876,12 +880,10 @@ hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int
   if (hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tT), sizeof(double2) * (size_t)G * A, st)) return e;
   hipLaunchKernelGGL(k_steer_transpose, dim3((unsigned)((G * A + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const double2*>(steer64), G, A, tT);
-  if (music)
-    hipLaunchKernelGGL(k_doa_fixup<true>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
-                       ncell_dev, ncell_host, G, tT, out_idx, out_gmax);
-  else
-    hipLaunchKernelGGL(k_doa_fixup<false>, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc,
-                       ncell_dev, ncell_host, G, tT, out_idx, out_gmax);
+  auto kern = A <= 8 ? (music ? k_doa_fixup<8, true> : k_doa_fixup<8, false>)
+                     : (music ? k_doa_fixup<16, true> : k_doa_fixup<16, false>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, G,
+                     tT, out_idx, out_gmax);
   const hipError_t e = hipGetLastError();
   const hipError_t f = hipFreeAsync(tT, st);
   return e != hipSuccess ? e : f;
