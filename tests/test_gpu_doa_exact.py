@@ -1,0 +1,81 @@
+"""Exact DoA argmax on every scan path (round 4): the grid index of each cell must be the fp64 argmax of
+its own fp32 signature, with keys within 1e-12 relative counted as ties won by the lower index (np.argmax on an exact
+tie).  The signatures are built to land on the cases the scans' rounding cannot decide and the re-scan must:
+  - perfect steering vectors at grid points (MUSIC: den = M - P <= 1e-12 there, so the reference's rule moves the
+    argmax to another point: angle_estimation.py:149-152);
+  - the +-90 degree pair (identical steering vectors at d = lambda / 2: an exact tie, lower index);
+  - signatures peaked halfway (in phase) between two grid points, inside a 32-point tile and across a tile boundary
+    (a near-tie the f16 / f32 scans cannot order);
+  - random signatures.
+Paths: the fused Toeplitz scan with ESPRIT / phase (rsl_doa_extras), the Toeplitz argmax (rsl_doa fast), the f32
+[Re; Im] scan (rsl_doa fast=False) and the f32 scan with the spectrum (k_doa_scan)."""
+import numpy as np
+import pytest
+import torch
+
+import radar_oracle as O
+
+pytestmark = pytest.mark.gpu
+TIE = 1e-12
+
+
+def _expected(sig32, steer, method):
+    s = sig32.astype(np.complex128)
+    s = s / np.linalg.norm(s, axis=1, keepdims=True)
+    P = np.abs(s @ steer.conj().T) ** 2
+    M = steer.shape[1]
+    key = np.where(M - P > 1e-12, P, -1.0) if method == 'music' else P
+    best = key.max(axis=1, keepdims=True)
+    cand = key >= best - TIE * np.abs(best)
+    return cand.argmax(axis=1)  # lowest index among the (near-)maxima
+
+
+def _signatures(A, grid, rs):
+    phi = np.pi * np.sin(np.radians(grid))
+    m = np.arange(A)
+    sig = []
+    for g in (0, 5, 31, 32, 100, 180, 359, 360):  # perfect steering vectors (MUSIC near-M cells), +-90 included
+        sig.append(np.exp(1j * phi[g] * m))
+    for g in (0, 360):  # the +-90 pair with a little noise: still an exact tie between indices 0 and 360
+        sig.append(np.exp(1j * phi[g] * m) + 1e-3 * (rs.randn(A) + 1j * rs.randn(A)))
+    for g in (10, 15, 31, 63, 95, 150, 200, 287, 300, 340):  # halfway in phase between g and g + 1 (31, 63, 95, 287:
+        mid = 0.5 * (phi[g] + phi[g + 1])  # across a 32-point tile boundary)
+        for amp in (0.0, 1e-3):
+            sig.append(np.exp(1j * mid * m) + amp * (rs.randn(A) + 1j * rs.randn(A)))
+    sig += list(rs.randn(200, A) + 1j * rs.randn(200, A))
+    return np.array(sig).astype(np.complex64)
+
+
+@pytest.mark.parametrize('A', [8, 4, 16])
+@pytest.mark.parametrize('method', ['music', 'beamforming'])
+def test_exact_argmax_every_path(ctx, A, method):
+    import rsl
+    rs = np.random.RandomState(100 + A)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=64, chirp_duration=25.6e-6, method=method)
+    ch = rsl.RadarChain(cfg, 1, ctx)
+    grid = O.azimuth_grid()
+    steer = O.steering_matrix(grid, A)
+    sig = _signatures(A, grid, rs)
+    n = len(sig)
+    S, C = ch.S, ch.C
+    cells = rs.choice(S * C, n, replace=False).astype(np.int32)
+    rds = np.zeros((1, A, S, C), np.complex64)
+    rds[0, :, cells // C, cells % C] = sig
+    d_rds = ctx.to_dev(rds)
+    c_frame = ctx.to_dev(np.zeros(n, np.int32))
+    c_rc = ctx.to_dev(cells)
+    want = _expected(sig, steer, method)
+    got = {}
+    if ch.steer['toeplitz']:
+        idx = ctx.empty((n,), torch.int32)
+        ctx.doa_extras(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n, esprit_scale=ch.esprit_scale, out_idx=idx,
+                       esprit=ctx.empty((n,), torch.float64), phase=ctx.empty((n,), torch.float64))
+        got['toeplitz+extras'] = idx
+        got['toeplitz'] = ctx.doa(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n)[0]
+    got['f32'] = ctx.doa(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n, fast=False)[0]
+    got['f32+spectrum'] = ctx.doa(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n, fast=False, want_spec=True)[0]
+    torch.cuda.synchronize()
+    for path, t in got.items():
+        g = t.cpu().numpy()[:n]
+        bad = np.nonzero(g != want)[0]
+        assert len(bad) == 0, (path, [(int(i), int(g[i]), int(want[i])) for i in bad[:8]])
