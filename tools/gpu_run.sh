@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-4 GPU session driver: each step under its own time limit; a step that times out, aborts or faults
 # (exit 124 / 134 / 137 / 139) ends the session (nothing more runs on the GPU), a failing test does not.
+# Steps on the development library (doavar, fixcount, k1cap, mall) need `make -C radar-slam_amd/csrc dev` first, the
+# ab steps `tools/build_ab.sh <commit>`.
 # usage: bash tools/gpu_run.sh TAG step...   steps: tests | testsall | fixcount | smoke | diag | bench | benchq | doactr | prof | ab | chunk | k1cap | mall
 set -u
 TAG=$1; shift
