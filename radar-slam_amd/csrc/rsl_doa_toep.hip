@@ -636,11 +636,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
     // the lane is below theta, so i is its exact argmax; n >= 2, a tile maximum of another tile >= theta, or a
     // non-positive best (a zero signature): ambiguous, re-scanned in fp64 below.
     // (any / two as lane masks: scalar ALU work, only the compares and the index selects are vector instructions)
+    constexpr float kAmb = DBG == 16 ? 1e-6f : kAmbRel;  // DBG 16 (development study): a tighter bound
     int i0 = 15, i1 = 15;
     bool any0 = false, two0 = false, any1 = false, two1 = false;
     {
       const floatx16 r0 = __builtin_bit_cast(floatx16, sv0), r1 = __builtin_bit_cast(floatx16, sv1);
-      const float th0 = best0 * (1.f - kAmbRel), th1 = best1 * (1.f - kAmbRel);
+      const float th0 = best0 * (1.f - kAmb), th1 = best1 * (1.f - kAmb);
 #pragma unroll
       for (int i = 15; i >= 0; --i) {
         const bool g0 = r0[i] >= th0, g1 = r1[i] >= th1;
@@ -654,8 +655,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
         any1 = any1 || g1;
       }
     }
-    bool amb0 = !any0 || two0 || second0 >= best0 * (1.f - kAmbRel) || !(best0 > 0.f);
-    bool amb1 = !any1 || two1 || second1 >= best1 * (1.f - kAmbRel) || !(best1 > 0.f);
+    bool amb0 = !any0 || two0 || second0 >= best0 * (1.f - kAmb) || !(best0 > 0.f);
+    bool amb1 = !any1 || two1 || second1 >= best1 * (1.f - kAmb) || !(best1 > 0.f);
     int g0 = 32 * (bt01 & 0xFFFF) + 4 * h + (i0 & 3) + 8 * (i0 >> 2);
     int g1 = 32 * (bt01 >> 16) + 4 * h + (i1 & 3) + 8 * (i1 >> 2);
     // merge the two K-half lanes of each column (first index wins on ties); ambiguous if the winner is, or if the
@@ -675,12 +676,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       const float lo0 = tk0 ? best0 : ob0, lo1 = tk1 ? best1 : ob1;
       best0 = tk0 ? ob0 : best0;
       g0 = tk0 ? og0 : g0;
-      amb0 = (tk0 ? oa0 : amb0) || lo0 >= best0 * (1.f - kAmbRel);
+      amb0 = (tk0 ? oa0 : amb0) || lo0 >= best0 * (1.f - kAmb);
       best1 = tk1 ? ob1 : best1;
       g1 = tk1 ? og1 : g1;
-      amb1 = (tk1 ? oa1 : amb1) || lo1 >= best1 * (1.f - kAmbRel);
-      loc0 = fmaxf(second0, os0) < best0 * (1.f - kAmbRel);
-      loc1 = fmaxf(second1, os1) < best1 * (1.f - kAmbRel);
+      amb1 = (tk1 ? oa1 : amb1) || lo1 >= best1 * (1.f - kAmb);
+      loc0 = fmaxf(second0, os0) < best0 * (1.f - kAmb);
+      loc1 = fmaxf(second1, os1) < best1 * (1.f - kAmb);
       pbt = obt ^ bt01;  // the partner K half's record tiles
     }
     float best = h ? best1 : best0;  // own cell = column tile h
@@ -915,6 +916,7 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 13) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 13, 12, true>;  // no second tracking
         if (v == 14) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 14, 12, true>;  // no in-tile count
         if (v == 15) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 15, 12, true>;  // second by one min
+        if (v == 16) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 16, 12, true>;  // bound 1e-6 (study)
       }
     }
   }

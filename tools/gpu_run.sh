@@ -21,6 +21,7 @@ for step in "$@"; do
     testsall) run testsall 600 python -u -m pytest tests -m gpu -q --maxfail 12 --timeout 150 --timeout-method thread ;;
     doavar) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run doavar 300 python -u tools/doa_var_time.py 0
       RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run doavar_ab 200 python -u tools/doa_var_time.py 0 ;;
+    bound) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run bound 300 python -u tools/doa_bound_study.py ;;
     fixcount) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fixcount 200 python -u tools/doa_fix_count.py ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     diag)
