@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
 DIST = False  # a torch.distributed process group is up (set in main)
-PROFILE = os.path.join(ROOT, 'profiles', 'r4k_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r4n_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
