@@ -24,6 +24,7 @@ for step in "$@"; do
     place)  # compaction / offsets placement in the pipelined step (RSL_BENCH_EMIT_BACK 0 / 1 / 2), 2 rounds
       for r in 1 2; do for p in 0 1 2; do RSL_BENCH_EMIT_BACK=$p run place${p}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_place*.log ;;
+    k1align) run k1align 300 python -u tools/k1_align.py ;;
     bound) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run bound 300 python -u tools/doa_bound_study.py ;;
     fixcount) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fixcount 200 python -u tools/doa_fix_count.py ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
