@@ -1,12 +1,13 @@
 """Register / spill / occupancy report of every kernel in one .hip file (hipcc -Rpass-analysis=kernel-resource-usage),
-compiled with the Makefile's flags for that file.   python tools/regs.py radar-slam_amd/csrc/rsl_doa_toep.hip [filter]"""
+compiled with the Makefile's flags for that file.   python tools/regs.py radar-slam_amd/csrc/rsl_doa_toep.hip [filter] [--dev]"""
 import re
 import subprocess
 import sys
 
 src = sys.argv[1]
 filt = sys.argv[2] if len(sys.argv) > 2 else ''
-flags = ['-O3', '-std=c++17', '--offload-arch=gfx950', '-Rpass-analysis=kernel-resource-usage', '-c', src, '-o',
+dev = '--dev' in sys.argv[3:]  # the development build's variants (-DRSL_DEV_KNOBS)
+flags = (['-DRSL_DEV_KNOBS'] if dev else []) + ['-O3', '-std=c++17', '--offload-arch=gfx950', '-Rpass-analysis=kernel-resource-usage', '-c', src, '-o',
          '/tmp/_regs.o']
 if 'doa' in src:
     flags[:0] = ['-fno-slp-vectorize']
