@@ -40,5 +40,5 @@ for seed_batch in range(2):  # two different 2000-frame blocks (rank 0 / rank 1 
         torch.cuda.synchronize()
         out[dbg] = (ch.gidx[:nc].clone(), marked, t0.elapsed_time(t1) / 4)
     diff = int((out['0'][0] != out['16'][0]).sum().item())
-    print(f'block {seed_batch}: cells {nc}; marked 2e-6 {out["0"][1]} / 1e-6 {out["16"][1]}; '
+    print(f'block {seed_batch}: cells {nc}; marked shipping {out["0"][1]} / study {out["16"][1]}; '
           f'DoA {out["0"][2]:.3f} / {out["16"][2]:.3f} ms; cells whose index differs: {diff}', flush=True)
