@@ -447,8 +447,7 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     import torch
     import torch.distributed as dist
     import rsl
-    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=ridge,
-                          front_chunk=int(os.environ.get('RSL_BENCH_FRONT_CHUNK', '0')))
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, ridge=ridge)
     NS = max(1, streams)
     if F % NS:
         raise SystemExit('--frames-per-step must be a multiple of --streams')
@@ -575,7 +574,7 @@ def chain_rooflines(r, A, C, S, F, config):
                  else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
     per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
     flops = 3 * 2 * (2 * A - 1) * ncl * G
-    Ff = min(Fl, r['chains'][0].chunk)  # frames per K1 / K2 launch (ChainConfig.front_chunk)
+    Ff = Fl  # frames per K1 / K2 launch
     kbytes = kernel_bytes_k1k2(A, C, S, Ff)
 
     def entry(name, ms):
@@ -622,8 +621,6 @@ def chain_rooflines(r, A, C, S, F, config):
     out["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big if k in src_std}
     out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * (NS if k not in fft_names else Fl * NS / Ff)
                                  for k, v in kt.items() if v[1]}
-    if Ff < Fl:
-        out["front_chunk_frames"] = Ff
     if ks:
         out["kernel_ms_standalone"] = {k: v[0] / max(v[1], 1) for k, v in ks.items() if v[1]}
     return out

@@ -100,16 +100,6 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
                    void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group);
 
-/* rsl_rds_detect over the batch in chunks of chunk_frames frames (the last one shorter) through one chunk-sized work
- *     buffer: K1 -> K2 of each chunk back to back on the handle's stream, so that a chunk's range spectra (packed
- *     `work`, stored without the nt hint when a launch's `work` is <= 128 MiB) can be read from the 256 MiB Infinity
- *     Cache instead of HBM.  work must hold chunk_frames frames; every other argument and output as rsl_rds_detect
- *     (outputs bit-identical to it).  chunk_frames <= 0 or >= F: one rsl_rds_detect call. */
-int rsl_rds_detect_chunked(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
-                           const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo,
-                           int i_hi, void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group,
-                           int chunk_frames);
-
 /* Offsets for the order-preserving compaction of a8's peak list (antenna -> range -> doppler,
  * dechirp.py:246-271) and of the deduplicated (range, doppler) cells that DoA runs on.
  *     entry_row_off i32 [F*A*S], cell_row_off i32 [F*S], scratch i32 [F*S],
@@ -137,9 +127,10 @@ int rsl_peak_emit(rsl_handle h, const void* rds, const void* mask, const void* u
 /* Host helper: MFMA operand tables of a steering matrix.  steer_c128 is the host [G][M] complex128
  * matrix of AngleEstimator.generate_steering_vector (angle_estimation.py:92-107) over the azimuth grid
  * (angle_estimation.py:59-60).  rsl_steer_table_floats returns the float count of the table; the build
- * writes (1) the f32 [Re; Im] operand for v_mfma_f32_16x16x4_f32 (*ntiles = its 16-row tiles) and
+ * writes (1) the f32 [Re; Im] operand for v_mfma_f32_16x16x4_f32 (*ntiles = its 16-row tiles),
  * (2) the Toeplitz-form f16 hi/lo operand for v_mfma_f32_32x32x16_f16, valid when the steering matrix is a
- * uniform linear array (*flags |= RSL_STEER_TOEPLITZ). */
+ * uniform linear array (*flags |= RSL_STEER_TOEPLITZ), and (3) the fp64 matrix itself transposed, [M][G] complex128
+ * (the last 4 G M floats), which the exact fp64 re-scan of near-tie cells reads. */
 long long rsl_steer_table_floats(int G, int M);
 int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_out, int* ntiles, int* flags);
 
@@ -147,10 +138,11 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
  *     (angle_estimation.py:67-176, 227-251; robust_angle_estimation.py:236-245).
  *     Cells (c_frame, c_rc) index rds c64 [*, A, S, C]; n = min(*ncell_dev, ncell) if ncell_dev is non-null
  *     (ncell = the lists' capacity: an overflowed list is processed up to its capacity), else ncell.
- *     steer_tab = device copy of the rsl_steer_table_build output; steer_c128 = device fp64 [G][M][2]
- *     steering matrix (required: the exact fp64 re-scan of the cells whose top-2 gap in the f16 hi/lo or f32 scan
- *     is inside that scan's error bound, and of MUSIC's near-degenerate cells, so out_idx is the fp64 argmax of each
- *     cell's own signature; keys within 1e-12 relative count as ties and the lower index wins, as np.argmax).
+ *     steer_tab = device copy of the rsl_steer_table_build output (its fp64 section feeds the exact fp64 re-scan of
+ *     the cells whose top-2 gap in the f16 hi/lo or f32 scan is inside that scan's error bound, and of MUSIC's
+ *     near-degenerate cells, so out_idx is the fp64 argmax of each cell's own signature; keys within 1e-13 relative
+ *     count as ties and the lower index wins, as np.argmax); steer_c128 (device fp64 [G][M][2], nullable) is no
+ *     longer read by rsl_doa / rsl_doa_extras and is kept for ABI compatibility.
  *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; with out_spec it applies to the RSL_DOA_SPEC_BLOCKED layout
  *     without out_gmax, the other spectrum requests take the f32 scan).
  *     out_idx i32 [n] = first-index argmax over the G grid points; out_gmax f32 [n] (nullable) = |a^H s|^2
@@ -163,7 +155,6 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
 
 /* a11-a16 + a15 + a26 fused: the Toeplitz argmax of rsl_doa (requires RSL_STEER_TOEPLITZ) plus, from the same
  *     signature load, ESPRIT (f64 deg, nullable; angle_estimation.py:178-225, esprit_scale = lambda/(2 pi d))
- *     (steer_c128 required, as for rsl_doa)
  *     and the spatial phase angle(s1 conj(s0)) (f64, nullable; velocity_solver.py:136) of each cell.
  *     Returns RSL_ERR_UNSUPPORTED when the grid does not fit the Toeplitz path. */
 int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const void* c_frame, const void* c_rc,

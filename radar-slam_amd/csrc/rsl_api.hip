@@ -246,31 +246,6 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   return hip_check(h, e, "doppler_detect");
 }
 
-int rsl_rds_detect_chunked(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
-                           const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo,
-                           int i_hi, void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group,
-                           int chunk_frames) {
-  if (!h) return RSL_ERR_INVALID;
-  if (chunk_frames <= 0 || chunk_frames >= F)
-    return rsl_rds_detect(h, cube, F, A, C_total, chirp0, C, S, table, dc_removal, work, rds, thr_power, i_lo, i_hi,
-                          mask, row_count, db_map, peak_pow, peak_pow_group);
-  if (A <= 0 || S <= 0 || C <= 0) return fail(h, RSL_ERR_INVALID, "rsl_rds_detect_chunked: bad shape");
-  const int W = (C + 63) / 64;
-  const size_t per_cube = (size_t)A * C_total * S * sizeof(float2), per_rds = (size_t)A * S * C * sizeof(float2);
-  const size_t per_mask = (size_t)A * S * W * 8, per_rc = (size_t)A * S * 4, per_map = (size_t)A * S * C * 4;
-  for (int f0 = 0; f0 < F; f0 += chunk_frames) {
-    const int n = F - f0 < chunk_frames ? F - f0 : chunk_frames;
-    auto at = [&](const void* p, size_t per) -> void* {
-      return p ? (void*)((const unsigned char*)p + per * (size_t)f0) : nullptr;
-    };
-    if (int r = rsl_rds_detect(h, at(cube, per_cube), n, A, C_total, chirp0, C, S, table, dc_removal, work,
-                               at(rds, per_rds), thr_power, i_lo, i_hi, at(mask, per_mask), at(row_count, per_rc),
-                               at(db_map, per_map), at(peak_pow, per_map), peak_pow_group))
-      return r;
-  }
-  return RSL_OK;
-}
-
 int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double thr_power, int i_lo, int i_hi,
                void* mask, void* row_count, void* db_map, void* peak_pow) {
   if (!h) return RSL_ERR_INVALID;
@@ -358,9 +333,13 @@ static long long steer_toep_floats(int G, int M) {
   return nt * KB * 2 * 64 * 4;
 }
 
+// (3) the fp64 steering matrix transposed, steerT[m][g] (double2), for k_doa_fixup's coalesced exact re-scan; at a
+// 16-B aligned float offset (both sections before it are multiples of 4 floats)
+static long long steer_t64_offset(int G, int M) { return steer_f32_floats(G, M) + steer_toep_floats(G, M); }
+
 long long rsl_steer_table_floats(int G, int M) {
   if (G <= 0 || M <= 0) return 0;
-  return steer_f32_floats(G, M) + steer_toep_floats(G, M);
+  return steer_t64_offset(G, M) + 4LL * G * M;
 }
 
 int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* ntiles_out, int* flags_out) {
@@ -388,6 +367,12 @@ int rsl_steer_table_build(const double* steer, int G, int M, float* out, int* nt
   const int uni = rsl::toep_table_build(steer, G, M, reinterpret_cast<uint16_t*>(out + steer_f32_floats(G, M)),
                                         nullptr);
   if (flags_out) *flags_out = (uni && rsl::toep_table_fits(G, M)) ? RSL_STEER_TOEPLITZ : 0;
+  double* tT = reinterpret_cast<double*>(out + steer_t64_offset(G, M));
+  for (int m = 0; m < M; ++m)
+    for (int g = 0; g < G; ++g) {
+      tT[((size_t)m * G + g) * 2] = steer[((size_t)g * M + m) * 2];
+      tT[((size_t)m * G + g) * 2 + 1] = steer[((size_t)g * M + m) * 2 + 1];
+    }
   return RSL_OK;
 }
 
@@ -402,7 +387,8 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   if (base_method != RSL_METHOD_MUSIC && base_method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa: unknown method");
   const bool music = base_method == RSL_METHOD_MUSIC;
-  if (!steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa: needs the fp64 steering table (exact re-scan)");
+  (void)steer_c128;  // the exact re-scan reads the fp64 copy inside steer_tab (rsl_steer_table_build)
+  const double* steerT = reinterpret_cast<const double*>((const float*)steer_tab + steer_t64_offset(G, A));
   if (!ncell_dev && ncell <= 0) return RSL_OK;
   hipSetDevice(h->device);
   Scope sc(h, RSL_K_DOA_SCAN);
@@ -415,7 +401,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
     return hip_check(h,
                      rsl::launch_doa_toep(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
                                           (const int*)c_rc, (const long long*)ncell_dev, ncell, tp, nt32, G, music,
-                                          (const double*)steer_c128, (int*)out_idx, (float*)out_gmax, 0.0,
+                                          steerT, (int*)out_idx, (float*)out_gmax, 0.0,
                                           nullptr, nullptr, toep_spec ? (float*)out_spec : nullptr),
                      "doa_toep");
   }
@@ -436,7 +422,7 @@ int rsl_doa(rsl_handle h, const void* rds, int A, int S, int C, const void* c_fr
   return hip_check(h,
                    rsl::launch_doa_fixup(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame,
                                          (const int*)c_rc, (const long long*)ncell_dev, ncell, G, music,
-                                         (const double*)steer_c128, (int*)out_idx, (float*)out_gmax),
+                                         steerT, (int*)out_idx, (float*)out_gmax),
                    "doa_fixup");
 }
 
@@ -450,7 +436,8 @@ int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const voi
   if (method != RSL_METHOD_MUSIC && method != RSL_METHOD_BEAMFORMING)
     return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: unknown method");
   const bool music = method == RSL_METHOD_MUSIC;
-  if (!steer_c128) return fail(h, RSL_ERR_INVALID, "rsl_doa_extras: needs the fp64 steering table (exact re-scan)");
+  (void)steer_c128;  // the exact re-scan reads the fp64 copy inside steer_tab (rsl_steer_table_build)
+  const double* steerT = reinterpret_cast<const double*>((const float*)steer_tab + steer_t64_offset(G, A));
   if (!rsl::toep_table_fits(G, A))
     return fail(h, RSL_ERR_UNSUPPORTED, "rsl_doa_extras: grid too large for the Toeplitz path (use rsl_doa)");
   if (!ncell_dev && ncell <= 0) return RSL_OK;
@@ -462,7 +449,7 @@ int rsl_doa_extras(rsl_handle h, const void* rds, int A, int S, int C, const voi
   return hip_check(h,
                    rsl::launch_doa_toep(h->stream, (const float2*)rds, A, S, C, (const int*)c_frame, (const int*)c_rc,
                                         (const long long*)ncell_dev, ncell, tp, nt32, G, music,
-                                        (const double*)steer_c128, (int*)out_idx, (float*)out_gmax, esprit_scale,
+                                        steerT, (int*)out_idx, (float*)out_gmax, esprit_scale,
                                         (double*)esprit_deg, (double*)phase),
                    "doa_extras");
 }

@@ -188,9 +188,11 @@ RSL_DEV void swap32_u4(uint4& a, uint4& b) {
   b = make_uint4(bv[0], bv[1], bv[2], bv[3]);
 }
 
-// The cell's (frame, range * C + doppler) pair; past the end: cell 0 (its results are never stored).
-RSL_DEV int2 load_cell(const int* __restrict__ cfr, const int* __restrict__ crc, long long c, bool ok) {
-  const long long cc = ok ? c : 0;
+// The cell's (frame, range * C + doppler) pair; past the end: cell 0 (its results are never stored).  Cell indices are
+// 32-bit (the launchers check counts < 2^31 - 64): 64-bit per-lane indices pushed the scan loop past 128 VGPRs, and the
+// spills' reloads (s_waitcnt vmcnt(0)) waited out the signature prefetch of the next pass.
+RSL_DEV int2 load_cell(const int* __restrict__ cfr, const int* __restrict__ crc, int c, bool ok) {
+  const unsigned cc = ok ? (unsigned)c : 0u;
   return make_int2(cfr[cc], crc[cc]);
 }
 
@@ -212,7 +214,7 @@ RSL_DEV void load_sig_at(const float2* __restrict__ rds, int2 fr, int A, size_t 
 
 template <int MA>
 RSL_DEV void load_sig_c(const float2* __restrict__ rds, const int* __restrict__ cfr, const int* __restrict__ crc,
-                        long long c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
+                        int c, bool ok, int A, size_t plane, size_t fstride, float2 (&s)[MA]) {
   load_sig_at<MA>(rds, load_cell(cfr, crc, c, ok), A, plane, fstride, s);
 }
 
@@ -256,8 +258,10 @@ constexpr float kAmbRel = 1e-6f;
 // Ties of the exact scan: keys within this relative distance count as equal and the lower grid index wins, as
 // np.argmax does on an exact tie.  Such keys are equal in exact arithmetic up to fp64 rounding (the reference's own
 // fp64 noise decides between them, e.g. the identical steering vectors of -90 and +90 degrees at d = lambda / 2),
-// and the parity tests treat gaps <= 1e-12 as ties (tests/parity.py OWN_TIE_RGAP).
-constexpr double kTieRel = 1e-12;
+// and the parity tests treat gaps <= 1e-13 as ties (tests/parity.py OWN_TIE_RGAP).  fp64 rounding of the 2M-term
+// sums is ~1e-15 relative: 1e-13 still covers the +-90 degree alias pair (identical to 5.6e-15) without treating
+// real gaps of 1e-13..1e-12 as ties.
+constexpr double kTieRel = 1e-13;
 
 // Exact fp64 scan of ONE cell over grid points [g0, g1) by the whole wave (wave-uniform cell c): the key is P if
 // M - P > 1e-12 (MUSIC, angle_estimation.py:149-152) else -1, P for beamforming; first index of the maximum key, as
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
                                                   const double* __restrict__ steer64, int* __restrict__ out_idx,
-                                                  float* __restrict__ out_gmax, double esprit_scale,
+                                                  float* __restrict__ out_gmax, float esprit_scale, int esprit_clamp,
                                                   double* __restrict__ out_esprit, double* __restrict__ out_phase,
                                                   float* __restrict__ out_spec) {
   extern __shared__ uint4 tt[];  // the whole Toeplitz operand table (<= 64 KiB)
@@ -290,13 +294,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   const int nvec = ntiles * KB * 2 * 64;
   for (int x = threadIdx.x; x < nvec; x += 256) tt[x] = ttab[x];
   __syncthreads();
-  const long long ncell = list_count(ncell_dev, ncell_host);
+  const int ncell = (int)list_count(ncell_dev, ncell_host);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
-  const long long nch = (ncell + 63) >> 6;
-  const long long stride = (long long)gridDim.x * 4;
-  long long ch = (long long)blockIdx.x * 4 + wave;
+  const int nch = (ncell + 63) >> 6;
+  const int stride = (int)gridDim.x * 4;
+  int ch = (int)blockIdx.x * 4 + wave;
   const float mthr = ((float)A - 1e-4f) * kToepScale;
   // Two-level prefetch: the signature of the next pass is loaded during this pass from cell indices that were loaded
   // one pass earlier (index loads followed at once by the dependent signature loads stalled every pass for a full
@@ -305,16 +309,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   float2 ns[MA], ns2[PD2 ? MA : 1];
   int2 nidx = make_int2(0, 0);
   if (ch < nch) {
-    const long long c = ch * 64 + lane;
+    const int c = ch * 64 + lane;
     if constexpr (DBG == 3) {
 #pragma unroll
       for (int m = 0; m < MA; ++m) ns[m] = make_float2(0.1f * (lane + m), 0.2f * m - lane * 0.01f);
     } else {
       load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
-      const long long c2 = (ch + stride) * 64 + lane;
+      const int c2 = (ch + stride) * 64 + lane;
       if constexpr (PD2) {
         if (ch + stride < nch) load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns2);
-        const long long c4 = (ch + 2 * stride) * 64 + lane;
+        const int c4 = (ch + 2 * stride) * 64 + lane;
         if (ch + 2 * stride < nch) nidx = load_cell(cfr, crc, c4, c4 < ncell);
       } else {
         if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
@@ -337,20 +341,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       out_idx[pc] = pidx;
       if constexpr (GMAX) out_gmax[pc] = pgv;
     }
-    const long long c = ch * 64 + lane;  // this lane's own cell
-    const long long nx = ch + stride;
+    const int c = ch * 64 + lane;  // this lane's own cell
+    const int nx = ch + stride;
     if constexpr (PD2) {
 #pragma unroll
       for (int m = 0; m < MA; ++m) ns[m] = ns2[m];
       if (nx + stride < nch) {
         load_sig_at<MA>(rds, nidx, A, plane, fstride, ns2);
-        const long long c5 = (nx + 2 * stride) * 64 + lane;
+        const int c5 = (nx + 2 * stride) * 64 + lane;
         if (nx + 2 * stride < nch) nidx = load_cell(cfr, crc, c5, c5 < ncell);
       }
     } else if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
       if constexpr (DBG == 10) nidx = make_int2(0, nidx.y & 2047);  // ablation: L2-resident signatures
       load_sig_at<MA>(rds, nidx, A, plane, fstride, ns);
-      const long long c3 = (nx + stride) * 64 + lane;
+      const int c3 = (nx + stride) * 64 + lane;
       if (nx + stride < nch) nidx = load_cell(cfr, crc, c3, c3 < ncell);
     }
     float ar[MA], ai[MA];
@@ -379,8 +383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
           // fp32 asin (the input angle is fp32 already; tolerance 1e-3 rad).  For d >= lambda/2 the reference's
           // argument never exceeds 1 (|angle| <= pi): clamp the fp32 rounding of pi * scale there; for d < lambda/2
           // |x| > 1 gives NaN as in the reference.
-          float x = ang * (float)esprit_scale;
-          if (esprit_scale * 3.14159265358979323846 <= 1.0 + 1e-9) x = fminf(fmaxf(x, -1.f), 1.f);
+          float x = ang * esprit_scale;
+          if (esprit_clamp) x = fminf(fmaxf(x, -1.f), 1.f);
           out_esprit[c] = (double)(asinf(x) * 57.2957795130823208768f);
         }
         if (out_phase)
@@ -706,7 +710,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
       const int ta = (bt01 >> sh) & 0xFFFF, tb = (pbt >> sh) & 0xFFFF;
       bidx = -1 - (loc ? (1 << 28) | (ta << 14) | tb : 0);  // k_doa_fixup's window code
     }
-    pc = c < ncell ? (int)c : -1;
+    pc = c < ncell ? c : -1;
     pidx = bidx;
     pgv = gval;
   }
@@ -859,38 +863,22 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
   }
 }
 
-// steerT[m][g] = steer64[g][m] (fp64 complex), the fixup's coalesced layout
-__global__ void k_steer_transpose(const double2* __restrict__ steer64, int G, int A, double2* __restrict__ steerT) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x < G * A) {
-    const int g = x / A, m = x - g * A;
-    steerT[(size_t)m * G + g] = steer64[x];
-  }
-}
-
 hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                             const int* c_rc, const long long* ncell_dev, long long ncell_host, int G, int music,
-                            const double* steer64, int* out_idx, float* out_gmax) {
-  if (A < 1 || A > 16 || G >= (1 << 24)) return hipErrorInvalidValue;
+                            const double* steerT, int* out_idx, float* out_gmax) {
+  if (A < 1 || A > 16 || G >= (1 << 24) || !steerT) return hipErrorInvalidValue;
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_DOA_NOFIX"))  // measurement only: marked cells keep -1 - code
     if (atoi(e) == 1) return hipSuccess;
 #endif
   long long fb = (ncell_host + 4LL * kFixCells - 1) / (4LL * kFixCells);  // kFixCells cells per wave
   if (fb < 1) fb = 1;
-  // the transposed table lives for this call only (stream-ordered allocation: concurrent calls on other streams with
-  // other steering tables cannot race on it)
-  double2* tT = nullptr;
-  if (hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tT), sizeof(double2) * (size_t)G * A, st)) return e;
-  hipLaunchKernelGGL(k_steer_transpose, dim3((unsigned)((G * A + 255) / 256)), dim3(256), 0, st,
-                     reinterpret_cast<const double2*>(steer64), G, A, tT);
+  // steerT = the transposed fp64 table [A][G], built once with the steering tables (rsl_steer_table_build)
   auto kern = A <= 8 ? (music ? k_doa_fixup<8, true> : k_doa_fixup<8, false>)
                      : (music ? k_doa_fixup<16, true> : k_doa_fixup<16, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)fb), dim3(256), 0, st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, G,
-                     tT, out_idx, out_gmax);
-  const hipError_t e = hipGetLastError();
-  const hipError_t f = hipFreeAsync(tT, st);
-  return e != hipSuccess ? e : f;
+                     reinterpret_cast<const double2*>(steerT), out_idx, out_gmax);
+  return hipGetLastError();
 }
 
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, bool SPEC = false>
@@ -940,9 +928,13 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   constexpr long long ppw = 8;
   long long blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
   if (blocks < 1) blocks = 1;
+  // ESPRIT's asin argument is clamped to [-1, 1] for d >= lambda / 2, where the reference's argument never exceeds 1
+  // (|angle| <= pi) and only the fp32 rounding of pi * scale can; for d < lambda / 2, |x| > 1 gives NaN as in the
+  // reference
+  const int clamp = esprit_scale * 3.14159265358979323846 <= 1.0 + 1e-9;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, rds, A, S, C, c_frame, c_rc, ncell_dev,
-                     ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, esprit_scale, out_esprit, out_phase,
-                     out_spec);
+                     ncell_host, tab, ntiles, G, steer64, out_idx, out_gmax, (float)esprit_scale, clamp, out_esprit,
+                     out_phase, out_spec);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   // the exact re-scan of the marked cells
   return launch_doa_fixup(st, rds, A, S, C, c_frame, c_rc, ncell_dev, ncell_host, G, MUSIC, steer64, out_idx,
@@ -954,7 +946,7 @@ hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int 
                            int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
                            double esprit_scale, double* out_esprit, double* out_phase, float* out_spec) {
   if (A < 1 || A > 16 || (ntiles32 & 1) || ncell_host >= (1LL << 31) - 64) return hipErrorInvalidValue;
-  if (!steer64) return hipErrorInvalidValue;  // the exact fp64 re-scan of ambiguous cells
+  if (!steer64) return hipErrorInvalidValue;  // steerT: the exact fp64 re-scan of ambiguous cells
   if ((out_esprit || out_phase) && A < 2) return hipErrorInvalidValue;
   const long long max_blocks = ncell_dev ? 0 : (ncell_host + 255) / 256;  // 4 waves x 64 cells
   if (!ncell_dev && ncell_host <= 0) return hipSuccess;

@@ -1107,11 +1107,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     if constexpr (S == 512 && CB == 8) {
       if (wexp) {  // packed work (work_packed_supported): the register-form 16 x 32 transform
         if (C != 128) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 128
-        // a launch whose packed `work` fits well inside the 256 MiB Infinity Cache (a chunk of ChainConfig.front_chunk
-        // frames) stores it without the nt hint, so that K2, launched right after, can read it from the cache; a whole
-        // batch's `work` (GBs) streams past the cache either way and keeps the nt stores
-        const bool small = (size_t)F * A * C * S * 6 <= ((size_t)128 << 20);
-        kern = small ? k_range_fft_r512<true, 0, false> : k_range_fft_r512<true>;
+        kern = k_range_fft_r512<true>;
         lds_k = 0;  // static LDS only
       }
     }

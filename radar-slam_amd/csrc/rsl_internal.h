@@ -64,10 +64,10 @@ hipError_t launch_doa_scan(hipStream_t st, const float2* rds, int A, int S, int 
 // Exact fp64 re-scan of the cells a DoA scan marked ambiguous (out_idx < 0), rsl_doa_toep.hip k_doa_fixup.
 hipError_t launch_doa_fixup(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                             const int* c_rc, const long long* ncell_dev, long long ncell_host, int G, int music,
-                            const double* steer64, int* out_idx, float* out_gmax);
+                            const double* steerT, int* out_idx, float* out_gmax);
 hipError_t launch_doa_toep(hipStream_t st, const float2* rds, int A, int S, int C, const int* c_frame,
                            const int* c_rc, const long long* ncell_dev, long long ncell_host, const void* toep_tab,
-                           int ntiles32, int G, int music, const double* steer64, int* out_idx, float* out_gmax,
+                           int ntiles32, int G, int music, const double* steerT, int* out_idx, float* out_gmax,
                            double esprit_scale, double* out_esprit, double* out_phase, float* out_spec = nullptr);
 // Host: builds the Toeplitz operand table; returns 1 if the steering matrix is a uniform linear array.
 int toep_table_build(const double* steer_c128, int G, int M, uint16_t* out, int* ntiles32_out);

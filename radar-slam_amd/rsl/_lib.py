@@ -38,8 +38,6 @@ SIGNATURES = {
     'rsl_rds': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
     'rsl_rds_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_double, c_int,
                                c_int, _P, _P, _P, _P, POINTER(c_int)]),
-    'rsl_rds_detect_chunked': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_double,
-                                       c_int, c_int, _P, _P, _P, _P, POINTER(c_int), c_int]),
     'rsl_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_double, c_int, c_int, _P, _P, _P, _P]),
     'rsl_peak_offsets': (c_int, [_P, _P, _P, c_int, c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P]),
     'rsl_peak_emit': (c_int, [_P, _P, _P, _P, _P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, _P, c_longlong,

@@ -46,9 +46,6 @@ class ChainConfig:
     bounds: tuple = (-50.0, 50.0, -50.0, 50.0)
     entry_frac: float = 0.20                   # capacity: peak entries per cube cell (9.4 % measured)
     cell_frac: float = 1.00                    # capacity: unique cells per (range, doppler) cell (54-76 %)
-    front_chunk: int = 0                       # > 0: RDS + detection in chunks of this many frames through one
-                                               # chunk-sized `work` buffer (K1 -> K2 of a chunk back to back, so the
-                                               # range spectra can be served from the Infinity Cache; 0: one launch pair)
     spectrum: bool = False                     # also write the MUSIC / beamforming spectrum of every cell, f32
                                                # cell-blocked [cells / 32, G, 32] (rsl.runtime.spectrum_rows)
                                                # (angle_estimation.py:299 stores spectrum f64[G] per target)
@@ -96,8 +93,7 @@ class RadarChain:
         self.cell_cap = (int(math.ceil(cfg.cell_frac * F * S * C)) + 64 + 3) & ~3  # a multiple of 4 (16-B rows)
         e = self._guarded_empty if guard else ctx.empty
         W = (C + 63) // 64
-        self.chunk = cfg.front_chunk if 0 < cfg.front_chunk < F else F
-        self.work = e((self.chunk, A, C, S), torch.complex64)
+        self.work = e((F, A, C, S), torch.complex64)
         self.rds = e((F, A, S, C), torch.complex64)
         self.mask = e((F, A, S, W), torch.int64)
         self.row_count = e((F, A, S), torch.int32)
@@ -151,7 +147,7 @@ class RadarChain:
             return
         group = ctx.rds_detect(cube, self.table, self.thr_p, self.i_lo, self.i_hi, rds=self.rds, work=self.work,
                                mask=self.mask, row_count=self.row_count, peak_pow=self.peak_pow,
-                               dc_removal=cfg.dc_removal, chunk=self.chunk if self.chunk < self.F else 0)
+                               dc_removal=cfg.dc_removal)
         self._group = group
         if offsets:
             ctx.offsets(self.mask, self.row_count, self.C, bufs=self.offs)

@@ -115,26 +115,18 @@ class Context:
     # -- a7 + a8 fused -----------------------------------------------------------------------------
     def rds_detect(self, cube, table, thr_power: float, i_lo: int, i_hi: int, *, rds, work, mask, row_count,
                    peak_pow=None, db_map=None, chirp0: int = 0, num_chirps: Optional[int] = None,
-                   dc_removal: bool = True, chunk: int = 0):
+                   dc_removal: bool = True):
         """cube [F, A, Ct, S] -> rds [F, A, S, C] + detection outputs, Doppler FFT and detection in one kernel.
-        chunk > 0: in chunks of that many frames through a chunk-sized ``work`` (rsl_rds_detect_chunked).
         Returns the row grouping of ``peak_pow`` (pass it to ``emit``)."""
         F, A, Ct, S = cube.shape
         C = Ct - chirp0 if num_chirps is None else num_chirps
         group = ctypes.c_int(1)
         self._bind()
-        if 0 < chunk < F:
-            self.check(self.lib.rsl_rds_detect_chunked(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
-                                                       int(dc_removal), _ptr(work), _ptr(rds), float(thr_power),
-                                                       int(i_lo), int(i_hi), _ptr(mask), _ptr(row_count),
-                                                       _ptr(db_map), _ptr(peak_pow), ctypes.byref(group), int(chunk)),
-                       'rsl_rds_detect_chunked')
-        else:
-            self.check(self.lib.rsl_rds_detect(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
-                                               int(dc_removal), _ptr(work), _ptr(rds), float(thr_power), int(i_lo),
-                                               int(i_hi), _ptr(mask), _ptr(row_count), _ptr(db_map), _ptr(peak_pow),
-                                               ctypes.byref(group)),
-                       'rsl_rds_detect')
+        self.check(self.lib.rsl_rds_detect(self.h, _ptr(cube), F, A, Ct, chirp0, C, S, _ptr(table),
+                                           int(dc_removal), _ptr(work), _ptr(rds), float(thr_power), int(i_lo),
+                                           int(i_hi), _ptr(mask), _ptr(row_count), _ptr(db_map), _ptr(peak_pow),
+                                           ctypes.byref(group)),
+                   'rsl_rds_detect')
         return int(group.value)
 
     # -- a8 -------------------------------------------------------------------------------------

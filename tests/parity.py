@@ -22,7 +22,7 @@ RDS_ATOL_REL = 1e-5
 PEAK_RTOL = 2e-5
 DOA_RGAP = 1e-6
 DOA_FLIP_FRAC = 2e-4
-OWN_TIE_RGAP = 1e-12
+OWN_TIE_RGAP = 1e-13
 ESPRIT_TOL_DEG = float(np.degrees(1e-3))
 VEL_COST_RTOL = 1e-6
 VEL_ATOL = 1e-4
@@ -120,7 +120,7 @@ def scan_flips(gpu_idx, gpu_sigs, steer, method='music'):
 def spectrum_argmax_consistent(spec, idx, method='music', atol=2e-5):
     """The grid index is a maximum of the written f32 spectrum up to the scan's precision: exactly the f16 scan's
     argmax where its top-2 gap is clear, the fp64 argmax of the cell's signature where it was re-scanned (a near-tie
-    inside the scan's 2e-6 bound), so the written value there is within the den / power tolerance of the row max."""
+    inside the scan's 1e-6 bound), so the written value there is within the den / power tolerance of the row max."""
     n = np.arange(len(idx))
     if method == 'music':
         d = np.where(spec > 0, 1.0 / np.where(spec > 0, spec, 1.0), np.inf)

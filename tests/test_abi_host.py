@@ -210,6 +210,27 @@ def test_context_requires_device():
         rsl.Context(0)
 
 
+def test_steer_table_fp64_transposed():
+    """The table's last section is the reference's fp64 steering matrix transposed, steerT[m][g] (complex128), at a
+    16-B aligned offset: k_doa_fixup's exact re-scan reads it (built once here instead of per rsl_doa call)."""
+    import rsl
+    lib = rsl.load()
+    for G, M in ((361, 8), (181, 16), (91, 4)):
+        st = O.steering_matrix(O.azimuth_grid(search_resolution=180.0 / (G - 1)), M)
+        assert st.shape == (G, M)
+        n = lib.rsl_steer_table_floats(G, M)
+        out = np.zeros(n, np.float32)
+        nt, fl = ctypes.c_int(), ctypes.c_int()
+        flat = np.ascontiguousarray(st).view(np.float64)
+        assert lib.rsl_steer_table_build(flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), G, M,
+                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(nt),
+                                         ctypes.byref(fl)) == 0
+        off = n - 4 * G * M
+        assert off % 4 == 0
+        tT = out[off:].view(np.complex128).reshape(M, G)
+        assert np.array_equal(tT, st.T)
+
+
 def _toeplitz_rows(lib, st):
     """Decode the Toeplitz f16 hi/lo section of the steering table into T_hi, T_lo [rows, 16*KB]."""
     G, M = st.shape
@@ -223,7 +244,8 @@ def _toeplitz_rows(lib, st):
     KB = 1 if M <= 8 else 2
     nt32 = (G + 31) // 32
     nt32 += nt32 & 1
-    h = out[nt.value * 64 * 4 * (1 if M <= 8 else 2):].view(np.float16).reshape(nt32, KB, 2, 64, 8)
+    o = nt.value * 64 * 4 * (1 if M <= 8 else 2)
+    h = out[o:o + nt32 * KB * 2 * 64 * 4].view(np.float16).reshape(nt32, KB, 2, 64, 8)
     T = np.zeros((2, nt32 * 32, 16 * KB))
     for t in range(nt32):
         for kb in range(KB):

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Round-4 GPU session driver: each step under its own time limit; a step that times out, aborts or faults
+# GPU session driver: each step under its own time limit; a step that times out, aborts or faults
 # (exit 124 / 134 / 137 / 139) ends the session (nothing more runs on the GPU), a failing test does not.
 # Steps on the development library (doavar, fixcount, k1cap, mall) need `make -C radar-slam_amd/csrc dev` first, the
 # ab steps `tools/build_ab.sh <commit>`.
-# usage: bash tools/gpu_run.sh TAG step...   steps: tests | testsall | fixcount | smoke | diag | bench | benchq | doactr | prof | ab | chunk | k1cap | mall
+# usage: bash tools/gpu_run.sh TAG step...   steps: tests | testsall | fixcount | smoke | bench | benchq | doactr | prof | ab | k1cap
 set -u
 TAG=$1; shift
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 stop() { echo "step $1 ended with $2: stopping"; exit $2; }
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -27,11 +28,11 @@ for step in "$@"; do
     k1align) run k1align 300 python -u tools/k1_align.py ;;
     bound) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run bound 300 python -u tools/doa_bound_study.py ;;
     fixcount) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fixcount 200 python -u tools/doa_fix_count.py ;;
+    probe)  # hipEvent semantics (tools/event_probe.hip), alone and under the kernel trace
+      run probe 60 ./tools/event_probe
+      run probe_trace 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_probe_trace -o t -- ./tools/event_probe ;;
+    transient) run transient 120 python -u tools/transient_row.py ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
-    diag)
-      for i in 1 2 3 4 5 6; do run diag_ng$i 90 python -u tools/pipelined_repeat.py 2 noguard; done
-      for i in 1 2; do run diag_g$i 90 python -u tools/pipelined_repeat.py 2; done
-      grep -h "mismatching\|placement" gpurun_out/${TAG}_diag_*.log ;;
     bench) run bench 400 python -u bench.py ;;
     benchq) run benchq 300 python -u bench.py --no-cpu-baseline --no-pcie --no-extra ;;
     doactr) F=1000 REPS=3 run doactr 400 bash tools/doa_counters.sh ;;
@@ -42,16 +43,10 @@ for step in "$@"; do
         run ab_new$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab_*.log ;;
-    chunk)  # the chained front half in chunks of N frames (ChainConfig.front_chunk), product nt work stores
-      for n in 0 16 32; do RSL_BENCH_FRONT_CHUNK=$n run chunk$n 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
-      python3 tools/ab_summary.py gpurun_out/${TAG}_chunk*.log ;;
     k1cap)  # resident K1 workgroups per CU capped (dev library, RSL_K1_WG_PER_CU): room for the back stream
       for r in 1 2; do
         for n in 0 2; do RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_K1_WG_PER_CU=$n run k1cap${n}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_k1cap*.log ;;
-    mall)
-      RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run mall_nt 240 python -u tools/chunk_mall2.py
-      RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_TEMPORAL=1 run mall_tmp 240 python -u tools/chunk_mall2.py ;;
   esac
 done
