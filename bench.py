@@ -539,6 +539,7 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     if collective:
         elapsed = _sync_max(elapsed, dev)
     kt = ctx.timing_read() if timing else {}
+    spans = ctx.timing_spans() if timing else {}  # per launch [start, end] on one device clock (the live timeline)
     ks = {}  # standalone kernel times: the pipelined timed region overlaps the two halves of consecutive batches
     if kt and pipeline and standalone:
         ctx.timing_reset()
@@ -550,8 +551,31 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     counted = chains[:1] if pipeline else chains  # pipelined: both buffers hold a full batch
     ne = sum(ch.totals()[0] for ch in counted)
     nc = sum(ch.totals()[1] for ch in counted)
-    return dict(elapsed=elapsed, kt=kt, ks=ks, ne=ne, nc=nc, NS=NS, G=len(chains[0].grid), cubes=cubes,
+    return dict(elapsed=elapsed, kt=kt, ks=ks, spans=spans, ne=ne, nc=nc, NS=NS, G=len(chains[0].grid), cubes=cubes,
                 chains=chains, reducer=reducer)
+
+
+def live_timeline(spans, steps):
+    """The unprofiled live timeline from the per-launch hipEvent spans of the timed steps (rsl_timing_spans): for each
+    scope its per-launch durations (median and range), and one step (the middle one) laid out against the start of
+    that step's range FFT, so the two streams' overlap can be read off (events time a scope from the later of its
+    stream's previous command and the cross-stream wait in front of it, to the end of its last kernel)."""
+    if not spans or 'range_fft' not in spans:
+        return None
+    out = {"what": "hipEvent spans of the timed steps (per launch): the unprofiled schedule", "scopes": {}}
+    for k, v in spans.items():
+        d = sorted(b - a for a, b in v)
+        out["scopes"][k] = {"launches": len(d), "median_ms": d[len(d) // 2], "min_ms": d[0], "max_ms": d[-1]}
+    i = len(spans['range_fft']) // 2
+    t0 = spans['range_fft'][i][0]
+    step = {}
+    for k, v in spans.items():
+        near = [(a - t0, b - t0) for a, b in v if -12.0 < a - t0 < 12.0]
+        if near:
+            step[k] = [[round(a, 3), round(b, 3)] for a, b in near]
+    out["step_ms_relative_to_range_fft_start"] = step
+    out["spans_ms"] = {k: [[round(a, 3), round(b, 3)] for a, b in v] for k, v in spans.items()}
+    return out
 
 
 def chain_rooflines(r, A, C, S, F, config):
@@ -734,6 +758,9 @@ def main():
         "peaks_per_frame": ne / F, "cells_per_frame": nc / F,
     }
     line.update(chain_rooflines(r, A, C, S, F, args.config))
+    tl = live_timeline(r.get('spans'), args.steps)
+    if tl:
+        line["live_timeline"] = tl
     if args.config == 'cfg2':
         # whole-chain HBM traffic per frame (committed PMC profile) beside the chain's algorithmic bytes (SURVEY §8d:
         # FFT stage 2 A C S 8 B + the DoA signature gather 8 M N_p)

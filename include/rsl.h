@@ -70,6 +70,10 @@ int rsl_fft_supported(int n);
 int rsl_timing_enable(rsl_handle h, int on);
 int rsl_timing_reset(rsl_handle h);
 int rsl_timing_read(rsl_handle h, int kernel_id, double* total_ms, long long* launches);
+/* The launches of one kernel id since the last rsl_timing_reset: [start, end] of each, in ms after an event that the
+ * reset recorded on the handle's stream (one device clock for every stream the handle ran on), in launch order.
+ * Writes min(n, max) pairs (nullable arrays) and returns n, the launch count (-1 on a bad argument). */
+int rsl_timing_spans(rsl_handle h, int kernel_id, int max, double* start_ms, double* end_ms);
 
 /* a7  SignalPreprocessor.generate_range_doppler_spectrum  (dechirp.py:168-213, incl. process_chirp
  *     :143-166, dechirp_signal :122-141, apply_window :85-108, remove_dc :110-120, chirp_subset :183-187).

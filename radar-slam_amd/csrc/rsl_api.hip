@@ -24,6 +24,10 @@ struct rsl_context {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   double ms[RSL_K_COUNT] = {0};
   long long cnt[RSL_K_COUNT] = {0};
+  // per-launch [start, end] in ms after the reference event t0 (recorded by rsl_timing_reset on the handle's stream):
+  // the live timeline of the launches since the reset, every stream's launches on one device clock
+  hipEvent_t t0 = nullptr;
+  std::vector<std::pair<double, double>> span[RSL_K_COUNT];
 };
 
 namespace {
@@ -87,6 +91,12 @@ void collect(rsl_context* h) {
       hipEventElapsedTime(&ms, p.first, p.second);
       h->ms[k] += ms;
       h->cnt[k] += 1;
+      if (h->t0) {
+        float a = 0.f, b = 0.f;
+        hipEventElapsedTime(&a, h->t0, p.first);
+        hipEventElapsedTime(&b, h->t0, p.second);
+        h->span[k].push_back({a, b});
+      }
       h->ev_pool.push_back(p);
     }
     h->ev[k].clear();
@@ -133,6 +143,7 @@ int rsl_destroy(rsl_handle h) {
     hipEventDestroy(p.first);
     hipEventDestroy(p.second);
   }
+  if (h->t0) hipEventDestroy(h->t0);
   delete h;
   return RSL_OK;
 }
@@ -163,8 +174,23 @@ int rsl_timing_reset(rsl_handle h) {
   for (int k = 0; k < RSL_K_COUNT; ++k) {
     h->ms[k] = 0;
     h->cnt[k] = 0;
+    h->span[k].clear();
   }
+  hipSetDevice(h->device);
+  if (!h->t0) hipEventCreate(&h->t0);
+  hipEventRecord(h->t0, h->stream);
   return RSL_OK;
+}
+
+int rsl_timing_spans(rsl_handle h, int kid, int max, double* start_ms, double* end_ms) {
+  if (!h || kid < 0 || kid >= RSL_K_COUNT || max < 0) return -1;
+  collect(h);
+  const int n = (int)h->span[kid].size();
+  for (int i = 0; i < n && i < max; ++i) {
+    if (start_ms) start_ms[i] = h->span[kid][i].first;
+    if (end_ms) end_ms[i] = h->span[kid][i].second;
+  }
+  return n;
 }
 
 int rsl_timing_read(rsl_handle h, int kid, double* total_ms, long long* launches) {

@@ -35,6 +35,7 @@ SIGNATURES = {
     'rsl_timing_enable': (c_int, [_P, c_int]),
     'rsl_timing_reset': (c_int, [_P]),
     'rsl_timing_read': (c_int, [_P, c_int, POINTER(c_double), POINTER(c_longlong)]),
+    'rsl_timing_spans': (c_int, [_P, c_int, c_int, POINTER(c_double), POINTER(c_double)]),
     'rsl_rds': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
     'rsl_rds_detect': (c_int, [_P, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_double, c_int,
                                c_int, _P, _P, _P, _P, POINTER(c_int)]),

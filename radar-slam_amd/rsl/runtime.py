@@ -96,6 +96,20 @@ class Context:
             out[name] = (ms.value, n.value)
         return out
 
+    def timing_spans(self) -> Dict[str, list]:
+        """Per kernel id: [(start_ms, end_ms), ...] of every launch since timing_reset, on one device clock (ms after
+        the reset's reference event), in launch order."""
+        out = {}
+        if not hasattr(self.lib, 'rsl_timing_spans'):  # an older library under RSL_LIBRARY (A/B runs)
+            return out
+        for k, name in enumerate(_lib.K_NAMES):
+            n = self.lib.rsl_timing_spans(self.h, k, 0, None, None)
+            if n > 0:
+                a, b = (c_double * n)(), (c_double * n)()
+                self.lib.rsl_timing_spans(self.h, k, n, a, b)
+                out[name] = list(zip(a, b))
+        return out
+
     # -- a7 -------------------------------------------------------------------------------------
     def rds(self, cube, table, *, chirp0: int = 0, num_chirps: Optional[int] = None, dc_removal: bool = True,
             out=None, work=None):

@@ -1,6 +1,6 @@
 """SHA-256 of every output of one cfg2 chain batch (RDS, masks, row counts, peak powers, offsets, lists, DoA, ESPRIT,
 phase, velocity) under the library RSL_LIBRARY: equal hashes across two libraries = bit-identical chains.
-GPU box:  RSL_LIBRARY=... python tools/chain_hash.py"""
+GPU box:  [CFG=cfg1|cfg2|cfg5] [F=frames] RSL_LIBRARY=... python tools/chain_hash.py"""
 import hashlib
 import json
 import os
@@ -13,11 +13,12 @@ import torch  # noqa: E402
 import rsl  # noqa: E402
 from bench import make_cubes  # noqa: E402
 
+A, C, TC = {'cfg1': (8, 64, 25.6e-6), 'cfg2': (8, 128, 51.2e-6), 'cfg5': (16, 256, 102.4e-6)}[os.environ.get('CFG', 'cfg2')]
 F = int(os.environ.get('F', '200'))
 ctx = rsl.get_context(0)
-cfg = rsl.ChainConfig(num_antennas=8, num_chirps=128, chirp_duration=51.2e-6)
+cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)
 ch = rsl.RadarChain(cfg, F, ctx)
-cube = make_cubes(ctx, 1, F, 8, 128, 51.2e-6, 0)[0]
+cube = make_cubes(ctx, 1, F, A, C, TC, 0)[0]
 ch.run(cube)
 torch.cuda.synchronize()
 ne, nc = ch.totals()

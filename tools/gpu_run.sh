@@ -31,6 +31,15 @@ for step in "$@"; do
     probe)  # hipEvent semantics (tools/event_probe.hip), alone and under the kernel trace
       run probe 60 ./tools/event_probe
       run probe_trace 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_probe_trace -o t -- ./tools/event_probe ;;
+    hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
+      for c in cfg1 cfg2 cfg5; do
+        CFG=$c F=40 run hash_new_$c 120 python -u tools/chain_hash.py
+        CFG=$c F=40 RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run hash_old_$c 120 python -u tools/chain_hash.py
+      done
+      for c in cfg1 cfg2 cfg5; do tail -1 gpurun_out/${TAG}_hash_new_$c.log; tail -1 gpurun_out/${TAG}_hash_old_$c.log; done ;;
+    tve)  # live per-kernel time: rocprofv3 kernel trace and the bench's hipEvent spans of the same run
+      run tve_trace 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_tve -o trace -- python3 bench.py --no-cpu-baseline --no-pcie --no-extra
+      python3 tools/trace_vs_events.py $(find gpurun_out/${TAG}_tve -name '*kernel_trace.csv' | head -1) gpurun_out/${TAG}_tve_trace.log > gpurun_out/${TAG}_tve_cmp.log 2>&1; cat gpurun_out/${TAG}_tve_cmp.log ;;
     transient) run transient 120 python -u tools/transient_row.py ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python -u bench.py ;;
