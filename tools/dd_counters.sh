@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counter passes over the RDS kernels alone (tools/dd_only.py: K1 + K2), for bottleneck analysis.
 set -euo pipefail
-OUT=gpurun_out/dd_ctr
+OUT=${OUT:-gpurun_out/dd_ctr}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 P="python3 tools/dd_only.py"

@@ -31,6 +31,14 @@ for step in "$@"; do
     probe)  # hipEvent semantics (tools/event_probe.hip), alone and under the kernel trace
       run probe 60 ./tools/event_probe
       run probe_trace 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_probe_trace -o t -- ./tools/event_probe ;;
+    ab3)  # product vs librsl_ab1.so vs librsl_ab.so (tools/build_ab.sh), 2 rounds, one box
+      for r in 1 2; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run ab3_old$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_ab1.so run ab3_mid$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+        run ab3_new$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_ab3_*.log ;;
+    ddctr) OUT=gpurun_out/${TAG}_ddctr run ddctr 400 bash tools/dd_counters.sh ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
         CFG=$c F=40 run hash_new_$c 120 python -u tools/chain_hash.py
