@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -256,6 +257,20 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   // the first 3/4 of the c64-sized work buffer the caller provides; wexp is the launchers' packed-path switch)
   unsigned char* wexp =
       rsl::work_packed_supported(C, S) ? (unsigned char*)work + (size_t)F * A * C * S * 6 : nullptr;
+#ifdef RSL_DEV_KNOBS
+  if (const char* fe = getenv("RSL_FRONT_FUSED"); fe && atoi(fe) == 1 && wexp && chirp0 == 0 && C_total == C) {
+    // development study: K1 + K2 in one launch with the packed work in a per-XCD L2 ring (rsl_fft.hip k_front_r512)
+    Scope sc(h, RSL_K_RANGE_FFT);
+    e = rsl::launch_front_fused(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
+                                dc_removal, (float2*)work, (size_t)F * A * C * S * sizeof(float2), (float2*)rds,
+                                thr_power, i_lo, i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
+                                (float*)peak_pow, &group);
+    if (e != hipErrorNotSupported) {
+      if (peak_pow_group) *peak_pow_group = group;
+      return hip_check(h, e, "front_fused");
+    }
+  }
+#endif
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,

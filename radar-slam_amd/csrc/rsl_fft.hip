@@ -1071,6 +1071,270 @@ static hipError_t launch_k2d_r128(hipStream_t st, const float2* work, int F, int
   return hipGetLastError();
 }
 
+#ifdef RSL_DEV_KNOBS
+// ---------------------------------------------------------------------------------------------
+// Fused front half at the cfg2 shape (S = 512, C = 128, packed work): K1 and K2 in ONE persistent launch whose packed
+// range spectra never leave the XCD's L2.  Each workgroup reads its XCD from HW_REG_XCC_ID and works only on that XCD's
+// share of the slabs (slab = one (frame, antenna)), from that XCD's queue of items in the order
+//   block b: K1 tiles (slab b, class c), c < 16;  then K2 tiles (slab b - kFrD, 16-bin tile t), t < 32,
+// so a K2 item always waits on K1 items dealt before it (to running workgroups): no deadlock.  Slab b's 16 K1 tiles
+// go into ring slot b % kFrR of that XCD's ring (kFrR slabs x 384 KiB = 2.3 MiB per XCD, inside its 4 MiB L2); its
+// K2 tiles wait until the slot's done counter shows the 16 K1 tiles, and a K1 tile for slab b waits until the K2
+// tiles of slab b - kFrR have read the slot.  Visibility is the XCD's own L2: the producer's stores complete
+// (s_waitcnt vmcnt(0), barrier) before one lane's counter add; the consumer polls by an atomic (memory side, never a
+// stale L2 copy) and reads the ring with nt loads (MI355X_MICROARCH: nt loads bypass the CU's L1 and are served by
+// the XCD's L2, where plain and nt stores keep their lines), so a line another CU rewrote is never read from a stale
+// L1.  Producer and consumer of a slot are always on one XCD (both chose the slab from their own XCD's queue).
+// Every wait is bounded (an error word is set and the item proceeds: wrong results, never a hang).
+// Development builds only (RSL_FRONT_FUSED=1; tools/front_fused_check.py): bit-identical to K1 + K2 but SLOWER, 6.62
+// against 5.08 ms per 2000 cfg2 frames (round 5).  LDS (43 KiB) holds it at 3 workgroups per CU, and the K2 tiles, which
+// reach 5.2 us per tile only by running 8 per CU, then expose their ring-load latency; claiming one item ahead with
+// the next K1 item's cube loads in flight made it worse (8.18 ms: the s_waitcnt before each done-count also waits for
+// those loads).  DESIGN.md section 4.
+constexpr int kFrR = 6, kFrD = 2;
+struct FrQueue {  // one 128-B line per counter
+  unsigned head[8][32];
+  unsigned done[8][kFrR][32];
+  unsigned cons[8][kFrR][32];
+  unsigned err[32];
+};
+constexpr size_t kFrRingBytes = (size_t)8 * kFrR * 16 * kPkTile;
+
+RSL_DEV unsigned fr_poll(unsigned* p) { return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// lane 0 of the workgroup waits until *p >= target (bounded), then the workgroup passes a barrier
+RSL_DEV void fr_wait(unsigned* p, unsigned target, unsigned* err) {
+  if (threadIdx.x == 0) {
+    unsigned it = 0;
+    // ~2^20 polls of >= 128 cycles (>= 50 ms) per wait; once any wait has timed out no workgroup waits again, so a
+    // broken hand-off ends the launch quickly (with wrong results and the error word set)
+    while (fr_poll(p) < target && fr_poll(err) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 20)) {
+        atomicOr(err, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int DBG = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_front_r512(const float2* __restrict__ cube, int Ct, int c0, int nslab,
+                                                          const float2* __restrict__ table,
+                                                          const float2* __restrict__ tw, int dc,
+                                                          unsigned char* __restrict__ ring, FrQueue* __restrict__ q,
+                                                          float2* __restrict__ rds, float thr_f, int i_lo, int i_hi,
+                                                          unsigned long long* __restrict__ mask,
+                                                          int* __restrict__ row_count, float* __restrict__ pk_pow) {
+  constexpr int S = 512, CB = 8, C = 128;
+  __shared__ float2 ldtab[S];
+  __shared__ float2 ldtw[32 * kR512TwPitch];
+  __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // K1: stage exchange / output buffer; K2: its tile rows + exchange
+  static_assert(CB * kR512Obuf <= CB * 16 * kR512Pitch, "output buffer must fit in the exchange buffer");
+  static_assert(sizeof(float2) * 18 * kR128Pitch + 16 * 2 * 16 <= sizeof(float2) * CB * 16 * kR512Pitch,
+                "the K2 tile must fit in the exchange buffer");
+  __shared__ int s_item;
+  float2* obuf = xbuf;
+  const int tid = threadIdx.x;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const int x = (int)(xcc & 7u);
+  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
+  const int total = nx > 0 ? 48 * (nx + kFrD) : 0;
+  for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
+  for (int k = tid; k < 32 * 16; k += kThreads) {
+    const int jj = k >> 4, kk = k & 15;
+    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
+  }
+  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
+  for (;;) {
+    if (tid == 0) s_item = (int)atomicAdd(&q->head[x][0], 1u);
+    __syncthreads();
+    const int k = s_item;
+    __syncthreads();  // s_item is rewritten by the next claim
+    if (k >= total) break;
+    const int b = k / 48, r = k - 48 * (k / 48);
+    if (r < 16) {
+      // ---- K1 tile: chirp class r of slab b (k_range_fft_r512's body) ----
+      if (b >= nx) continue;
+      const int slot = b % kFrR;
+      fr_wait(&q->cons[x][slot][0], 32u * (unsigned)(b / kFrR), &q->err[0]);
+      // the thread index laundered per item: the compiler must not hoist this item's LDS table reads and addresses
+      // out of the item loop (they would stay live across the K2 items)
+      int lt = tid;
+      asm volatile("" : "+v"(lt));
+      const int row = lt >> 5, j = lt & 31;
+      const int k1b = (lt >> 1) & 15, h = lt & 1;
+      const int cb = r;
+      const long fa = (long)s0 + b;
+      float2 v[16];
+      {
+        const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 16 * row) * S + j;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = ld8<true>(src + 32 * m);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ldtab[j + 32 * m]);
+      }
+      Dft<16>::run(v);
+#pragma unroll
+      for (int kk = 1; kk < 16; ++kk) v[kk] = cmul(v[kk], ldtw[j * kR512TwPitch + kk]);
+      float2* xw = xbuf + row * 16 * kR512Pitch + j;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) xw[kk * kR512Pitch] = v[kk];
+      __syncthreads();
+      const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
+      Dft<16>::run(v);
+      float2 xo[16];
+      const rsl_f2v sgn = h ? (rsl_f2v){-1.f, -1.f} : (rsl_f2v){1.f, 1.f};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const float2 u = h ? cmul(v[kk], w32(kk)) : v[kk];
+        float2 recv;
+        recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0xB1, 0xF, 0xF, true));
+        recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0xB1, 0xF, 0xF, true));
+        xo[kk] = cf(__builtin_elementwise_fma(sgn, cv(u), cv(recv)));
+      }
+      if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
+      __syncthreads();  // xbuf reads done: obuf aliases it
+      float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) ow[16 * kk] = xo[kk];
+      __syncthreads();
+      float2 y0[8], y1[8];
+      const int pos = 2 * lt + (lt >= 128 ? 8 : 0);
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) {
+        const float4 ab = *reinterpret_cast<const float4*>(obuf + qq * kR512Obuf + pos);
+        y0[qq] = make_float2(ab.x, ab.y);
+        y1[qq] = make_float2(ab.z, ab.w);
+      }
+      Dft<8>::run(y0);
+      Dft<8>::run(y1);
+#pragma unroll
+      for (int kk = 1; kk < 8; ++kk) {
+        const float2 wk = tw[4 * cb * kk];
+        y0[kk] = cmul(y0[kk], wk);
+        y1[kk] = cmul(y1[kk], wk);
+      }
+      float f0[16], f1[16];
+      unsigned m0 = 0u, m1 = 0u;
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) {
+        f0[2 * qq] = y0[qq].x;
+        f0[2 * qq + 1] = y0[qq].y;
+        f1[2 * qq] = y1[qq].x;
+        f1[2 * qq + 1] = y1[qq].y;
+        m0 = max(m0, max(__float_as_uint(y0[qq].x) & 0x7FFFFFFFu, __float_as_uint(y0[qq].y) & 0x7FFFFFFFu));
+        m1 = max(m1, max(__float_as_uint(y1[qq].x) & 0x7FFFFFFFu, __float_as_uint(y1[qq].y) & 0x7FFFFFFFu));
+      }
+      const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+      uint4 w0[3], w1[3];
+      pk_pack16(f0, e0, w0);
+      pk_pack16(f1, e1, w1);
+      uint4* dst = reinterpret_cast<uint4*>(xring + ((size_t)slot * 16 + cb) * kPkTile) + lt;
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
+        st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's stores are in the L2 before the count
+      __syncthreads();  // obuf reads done (the next item rewrites it), every wave's stores waited for
+      if (tid == 0) __hip_atomic_fetch_add(&q->done[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      // ---- K2 tile: 16-bin tile r - 16 of slab b - kFrD (k_doppler_detect_r128's body) ----
+      const int bb = b - kFrD;
+      if (bb < 0 || bb >= nx) continue;
+      const int slot = bb % kFrR;
+      fr_wait(&q->done[x][slot][0], 16u * (unsigned)(bb / kFrR + 1), &q->err[0]);
+      constexpr int KB = 16, NR = KB + 2, NCB = 16, LD = kR128Pitch, SKL = kR128Skew, XPI = 8 * KB, XPH = 17;
+      float2* buf = xbuf;
+      float2* xi = buf;
+      float2* xh = buf + NCB * XPI;
+      const int k0 = (r - 16) * KB;
+      const unsigned fa = (unsigned)(s0 + bb);
+      const unsigned char* tiles = xring + (size_t)slot * 16 * kPkTile;
+      auto unit = [&](int kk, int cls, uint4(&w)[3]) {
+        const uint4* src = reinterpret_cast<const uint4*>(tiles + (size_t)cls * kPkTile +
+                                                          (size_t)(3 * (kk & 1)) * kPkPlane) + (kk >> 1);
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj)
+          w[jj] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + jj * (kPkPlane / 16))));
+      };
+      int lt = tid;
+      asm volatile("" : "+v"(lt));
+      const int bq = lt % KB, cls = lt / KB;
+      const bool halo = lt < 2 * NCB;
+      const int hside = lt >> 4, hcls = lt & 15;
+      // (wh and xv zero-initialised: an undefined value on the paths that skip them would be carried around the item
+      // loop in registers)
+      uint4 wi[3], wh[3] = {};
+      unit(k0 + bq, cls, wi);
+      if (halo) {
+        int kk = hside ? k0 + KB : k0 - 1;
+        kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+        unit(kk, hcls, wh);
+      }
+      auto stage1 = [&](const uint4(&w)[3], float2* d, int st) {
+        float f[16];
+        pk_unpack16(w, f);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) d[kk * st] = make_float2(f[2 * kk], f[2 * kk + 1]);
+      };
+      stage1(wi, xi + cls * XPI + bq, KB);
+      if (halo) stage1(wh, xh + hcls * XPH + hside, 2);
+      __syncthreads();  // every ring load of this tile has returned (its values are in LDS)
+      if (tid == 0) __hip_atomic_fetch_add(&q->cons[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool s2 = lt < 8 * NR;
+      const bool hs = lt >= 8 * KB;
+      const int k1 = hs ? (lt - 8 * KB) >> 1 : lt / KB;
+      const int b2 = hs ? ((lt & 1) ? NR - 1 : 0) : (lt % KB) + 1;
+      float2 xv[16] = {};
+      if (s2) {
+        const float2* src = hs ? xh + 2 * k1 + (lt & 1) : xi + lt;
+        const int cs = hs ? XPH : XPI;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) xv[c] = src[c * cs];
+        Dft<16>::run(xv);
+      }
+      __syncthreads();
+      if (s2) {
+        float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0);
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) rw[k1 + 8 * k2] = xv[k2];
+      }
+      __syncthreads();
+      dd_tile_compute_reg<C, KB, 256, 0, LD, false, SKL>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds,
+                                                         thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow, lt);
+      __syncthreads();  // the tile's LDS reads done before the next item reuses xbuf
+    }
+  }
+}
+
+// The fused front half (k_front_r512) when the caller's work buffer holds the ring and the queue (F A >= 40 slabs at
+// cfg2) and no dB map is requested; returns hipErrorNotSupported otherwise (the two-kernel path runs).
+hipError_t launch_front_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
+                              const float2* table, const float2* tw_S, int dc, float2* work, size_t work_bytes,
+                              float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
+                              float* dbmap, float* pk_pow, int* pk_group) {
+  if (S != 512 || C != 128 || dbmap) return hipErrorNotSupported;
+  const size_t need = kFrRingBytes + sizeof(FrQueue);
+  if (work_bytes < need || (long)F * A < 8 * (kFrD + 1)) return hipErrorNotSupported;
+  unsigned char* ring = reinterpret_cast<unsigned char*>(work);
+  FrQueue* q = reinterpret_cast<FrQueue*>(ring + kFrRingBytes);
+  if (hipError_t e = hipMemsetAsync(q, 0, sizeof(FrQueue), st)) return e;
+  auto kern = k_front_r512<>;
+  const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, 1L << 30);
+  *pk_group = 16;  // tile-compact peak powers, as k_doppler_detect_r128
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), 0, st, cube, Ct, c0, F * A, table, tw_S, dc,
+                     reinterpret_cast<unsigned char*>(ring), q, rds, threshold_as_float(thr_p), i_lo, i_hi, mask,
+                     row_count, pk_pow);
+  return hipGetLastError();
+}
+#endif  // RSL_DEV_KNOBS
+
 template <int C>
 static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
                              double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,

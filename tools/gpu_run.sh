@@ -39,6 +39,7 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab3_*.log ;;
     ddctr) OUT=gpurun_out/${TAG}_ddctr run ddctr 400 bash tools/dd_counters.sh ;;
+    fused) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fused 240 python -u tools/front_fused_check.py ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
         CFG=$c F=40 run hash_new_$c 120 python -u tools/chain_hash.py

@@ -11,9 +11,7 @@ checks them against the serial K1 output, and scores candidate mechanisms: e_j e
 between the right operand and some other register value (a stale value, the other half of a packed pair, a
 neighbouring lane's value).  CPU:  python tools/transient_fit.py"""
 import ast
-import itertools
 import os
-import re
 
 import numpy as np
 
@@ -36,7 +34,8 @@ print(f'rebuilt K1 row vs serial K1 output (bins 1..255): max rel err {err:.2e}'
 
 # recorded pipelined values (bins 16..31 = output k = 1 of butterflies j = 0..15)
 log = open(os.path.join(ROOT, 'gpurun_out', 'r4c_diag_g1.log')).read()
-vals = ast.literal_eval(re.search(r'\[index, serial, pipelined\]: (\[.*?\])\]?;', log).group(1) + ']')
+a = log.index('[index, serial, pipelined]: ') + len('[index, serial, pipelined]: ')
+vals = ast.literal_eval(log[a:log.index(']; batch', a) + 1])
 rec = {tuple(i)[3]: (s, p) for i, s, p in vals}
 h = 0.70710678118654752440
 e_obs = np.array([(rec[16 + j][1] - rec[16 + j][0]).real / h for j in range(R)])
