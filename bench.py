@@ -30,10 +30,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
 DIST = False  # a torch.distributed process group is up (set in main)
-PROFILE = os.path.join(ROOT, 'profiles', 'r4n_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r5g_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
+CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r5h_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
 STANDALONE_RUNS = 6  # unpipelined chain runs after the timed region (kernel_ms_standalone, fft_stage_standalone)
 TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
                   ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')
@@ -44,10 +45,11 @@ def pmc_traffic(kernel_prefix, frames_per_launch, config='cfg2'):
     MI355X_MICROARCH.md), scaled to this launch's frame count; None when no profile is present, the profile was
     collected on another workload or holds no kernel of that name (a kernel renamed or replaced since: the profile is
     stale for it, and its bytes are not reported)."""
-    if config != PROFILE_CONFIG:
+    path = {PROFILE_CONFIG: PROFILE, 'cfg5': CFG5_PROFILE}.get(config)
+    if path is None:
         return None
     try:
-        prof = json.load(open(PROFILE))
+        prof = json.load(open(path))
     except (OSError, ValueError):
         return None
     for name, e in prof.get('kernels', {}).items():
@@ -213,7 +215,7 @@ def cpu_baseline(procs=0, kmax=3000, vec_frames=2, ridge=0.01):
                                       f"{wall_vec:.1f} s wall"})
 
 
-SPEC_PROFILE = os.path.join(ROOT, 'profiles', 'r2b_spectrum_pmc.json')  # tools/profile_spectrum.sh
+SPEC_PROFILE = os.path.join(ROOT, 'profiles', 'r5g_spectrum_pmc.json')  # tools/profile_spectrum.sh
 
 
 def spectrum_traffic(frames):
@@ -422,7 +424,7 @@ def kernel_bytes_k1k2(A, C, S, F):
       K2 k_doppler_detect_r128: read the packed spectra of 16 + 2 halo range bins per 16-bin tile + write the c64 RDS
          (masks / peak powers, ~1 %, not counted)                                     = A C S (6 x 18 / 16 + 8) B/frame
     c64 `work` at other shapes (k_range_fft_p / k_doppler_detect): 2 A C S 8 B per frame each."""
-    if (C, S) == (128, 512):
+    if (C, S) in ((128, 512), (256, 1024)):  # packed (cfg2; cfg5: k_range_fft_r1024 / k_doppler_detect_r256, the same)
         return {'range_fft': A * C * S * 14.0 * F, 'doppler_fft': A * C * S * (6.0 * 18 / 16 + 8) * F}
     return {'range_fft': 2 * A * C * S * 8 * F, 'doppler_fft': 2 * A * C * S * 8 * F}
 
@@ -582,6 +584,8 @@ def chain_rooflines(r, A, C, S, F, config):
     """roofline (FFT stage, live), fft_stage_standalone, roofline_doa, kernel_rooflines_standalone and the per-kernel
     ms of one measure_chain result."""
     kt, ks, NS, G = r['kt'], r['ks'], r['NS'], r['G']
+    tsrc = TRAFFIC_SOURCE if config != 'cfg5' else TRAFFIC_SOURCE.replace(os.path.relpath(PROFILE, ROOT),
+                                                                          os.path.relpath(CFG5_PROFILE, ROOT))
     out = {}
     if not kt:
         return out
@@ -593,9 +597,9 @@ def chain_rooflines(r, A, C, S, F, config):
     #  K5 k_doa_toep: one real dot product of length 2M-1 per (cell, grid point) (Toeplitz form of |a^H s|^2),
     #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
     src_std = ks if ks else kt
-    packed = (C, S) == (128, 512)
-    fft_names = ({'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'} if packed
-                 else {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
+    fft_names = {(128, 512): {'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'},
+                 (256, 1024): {'range_fft': 'k_range_fft_r1024', 'doppler_fft': 'k_doppler_detect_r256'}}.get(
+        (C, S), {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
     per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
     flops = 3 * 2 * (2 * A - 1) * ncl * G
     Ff = Fl  # frames per K1 / K2 launch
@@ -608,14 +612,14 @@ def chain_rooflines(r, A, C, S, F, config):
             # after on the same stream): the rate is charged for both
             return {"bound": "mfma", "kernel": "k_doa_toep + k_doa_fixup", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                    "traffic": pmc_traffic('k_doa_toep', Fl, config), "traffic_source": TRAFFIC_SOURCE,
+                    "traffic": pmc_traffic('k_doa_toep', Fl, config), "traffic_source": tsrc,
                     "avg_launch_ms": ms, "algorithmic_flops_per_launch": flops,
                     "reference_equivalent_flops_per_launch": ncl * G * (8 * A + 5)}
         kern = fft_names[name]
         ach = kbytes[name] / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "kernel": kern, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, Ff, config),
-                "traffic_source": TRAFFIC_SOURCE, "avg_launch_ms": ms, "design_bytes_per_launch": kbytes[name],
+                "traffic_source": tsrc, "avg_launch_ms": ms, "design_bytes_per_launch": kbytes[name],
                 "note": "per-kernel design bytes (cube or work in, work or RDS out): the work round trip counts "
                         "here, so these fractions are kernel efficiencies, not the stage's algorithmic roofline"}
 
@@ -634,7 +638,7 @@ def chain_rooflines(r, A, C, S, F, config):
         return {"bound": "hbm", "kernels": [fft_names[k] for k in fft_k],
                 "achieved": fft_bytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": fft_bytes / t / 1e9 / HBM_PEAK_GBS,
-                "traffic": None if any(x is None for x in tr) else sum(tr), "traffic_source": TRAFFIC_SOURCE,
+                "traffic": None if any(x is None for x in tr) else sum(tr), "traffic_source": tsrc,
                 "avg_launch_ms": t * 1e3, "algorithmic_bytes_per_launch": fft_bytes, "timed": timed}
 
     out["roofline"] = stage(kt, "hipEvents over the timed region (pipelined: the stage co-runs with the previous "

@@ -146,9 +146,9 @@ RSL_DEV void pk_unpack16(const uint4 (&w)[3], float (&f)[16]) {
 }
 
 // Grid of a persistent kernel: resident workgroups only (occupancy x CUs), at most ntile.
-static long resident_grid(const void* kern, size_t lds, long ntile) {
+static long resident_grid(const void* kern, size_t lds, long ntile, int nt = kThreads) {
   int nb = 0, dev = 0, ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kThreads, lds) != hipSuccess || nb < 1) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, nt, lds) != hipSuccess || nb < 1) nb = 1;
   if (nb > 8) nb = 8;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -544,6 +544,190 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
 }
 
 // ---------------------------------------------------------------------------------------------
+// K1 for S = 1024 with packed `work` (the configs[4] shape: C = 256): k_range_fft_r512's design at
+// twice the length, on 512 threads.  A tile is chirp class c of one (frame, antenna), the 8 chirps c + 32 q (q < 8,
+// c < 32), so that the radix-8 step of the 256-point Doppler transform over q, with its W256^(c k1) twiddle, runs here
+// and K2 (k_doppler_detect_r256) does the 32-point step over the classes.  One wave per chirp row:
+//   x[n], n = j + 64 m (j < 64, m < 16): lane j of wave q loads x[j + 64 m] (8-B loads, 512-B runs), x conj(ref) w
+//   (the dechirp table is read through L1: in LDS it would not leave room for two workgroups per CU);
+//   stage 1: V[j][k1] = DFT16_m, times W1024^(j k1) (LDS, 16 per j, XOR-swizzled: k1 ^ ((j >> 1) & 15));
+//   exchange: V -> xbuf[q][k1][j ^ 4 k1] (the stage-2 reads of 32 lanes then hit 64 distinct banks, the writes 32);
+//   stage 2: lane (k1 = lane / 4, h = lane % 4) takes j = 4 i + h: F_h = DFT16_i, u_h = W64^(h k') F_h[k'], and the
+//   radix-4 step over h across the lane quad by two DPP swaps (h ^ 2, then h ^ 1 after the W4 twiddle), after which
+//   lane h holds Y[k' + 16 s], s = (h >> 1) | 2 (h & 1): bin k1 + 16 k' + 256 s;
+//   output: -> obuf[q][bin ^ 4 s] (conflict-free 16-lane writes), then thread p reads bins 2p, 2p + 1 of the 8 rows
+//   (16-B reads), takes W256^(c k1) DFT8_q and stores both bins packed (pk_pack16; planes of 512 pairs x 16 B).
+// LDS: xbuf 64 KiB (aliased by obuf) + twiddles 8 KiB: two workgroups (16 waves) per CU.
+constexpr int kR1kThreads = 512;
+constexpr int kPkPlane1k = 8 * 1024;        // bytes per plane of one S = 1024 tile (512 pairs x 16 B)
+constexpr int kPkTile1k = 6 * kPkPlane1k;   // bytes per tile
+RSL_DEV int r1k_tw(int j, int k) { return j * 16 + (k ^ ((j >> 1) & 15)); }  // W1024^(j k) in ldtw
+
+template <bool DYN, int DBG = 0>
+__global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_range_fft_r1024(const float2* __restrict__ cube, int A, int Ct,
+                                                                  int c0, int C, long ntile,
+                                                                  const float2* __restrict__ table,
+                                                                  const float2* __restrict__ tw, int dc,
+                                                                  float2* __restrict__ work, int slot,
+                                                                  unsigned char* __restrict__ wexp) {
+  constexpr int S = 1024, NT = kR1kThreads, ncb = 32;  // C = 256 wherever this kernel runs (work_packed_supported)
+  (void)wexp;
+  (void)C;
+  (void)A;
+  __shared__ float2 ldtab[S];
+  __shared__ float2 ldtw[64 * 16];
+  __shared__ float2 xbuf[8 * S];  // stage exchange; aliased by the output buffer
+  // 80 KiB exactly (two workgroups per CU): the tile hand-off word lives in a twiddle slot no lane reads (k1 = 0 of j = 0)
+  long* s_nn = reinterpret_cast<long*>(&ldtw[r1k_tw(0, 0)]);
+  float2* obuf = xbuf;
+  const int tid = threadIdx.x;
+  const long G = gridDim.x;
+  for (int k = tid; k < S; k += NT) ldtab[k] = table[k];
+  for (int k = tid; k < 64 * 16; k += NT) {
+    const int jj = k >> 4, kk = k & 15;
+    if (kk) ldtw[r1k_tw(jj, kk)] = tw[jj * kk];  // W1024^(j k1), j k1 <= 945 (k1 = 0: never read)
+  }
+  auto load = [&](float2(&nx)[16], long t) {
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 6, j = lt & 63;
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 32 * row) * S + j;  // chirp class cb, row q = row
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if constexpr (DBG == 2)
+        nx[m] = make_float2((float)tid, (float)m);
+      else
+        nx[m] = ld8<true>(src + 64 * m);
+    }
+  };
+  const int xcd = blockIdx.x & 7;
+  const long gx = (G - xcd + 7) / 8;
+  const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
+  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  __syncthreads();
+  auto body = [&](float2(&nx)[16], long t, long tn) {
+    unsigned claim = 0;
+    if (DYN && tid == 0) claim = atomicAdd(head, 1u);
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    // the thread index laundered per tile: otherwise the compiler hoists the tile-invariant table and twiddle reads
+    // out of the tile loop (92 registers live across it: 256 VGPRs with spills)
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 6, j = lt & 63;
+    const int k1b = (lt >> 2) & 15, h = lt & 3;
+    const int s_out = (h >> 1) | ((h & 1) << 1);  // the radix-4 output index lane h ends with
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 64 * m]);
+    load(nx, tn < hi ? tn : t);  // in flight during this tile's transforms and stores
+    if constexpr (DBG == 3) {
+      if (v[0].x == 1.2345e30f) work[tid] = v[1];
+      if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
+      __syncthreads();
+      return;
+    }
+    // stage 1: DFT16 over m, twiddle W1024^(j k1)
+    Dft<16>::run(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[r1k_tw(j, k)]);
+    float2* xw = xbuf + row * S;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xw[k * 64 + (j ^ ((4 * k) & 63))] = v[k];
+    __syncthreads();
+    // stage 2: DFT16 over i of V[4 i + h][k1], then the radix-4 step over h across the lane quad
+    const float2* xr = xbuf + row * S + k1b * 64;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xr[4 * (i ^ k1b) + h];
+    Dft<16>::run(v);
+    const float sg1 = (h & 2) ? -1.f : 1.f, sg2 = (h & 1) ? -1.f : 1.f;
+    __syncthreads();  // xbuf reads done: obuf aliases it (the radix-4 step below writes each output as it forms)
+    float2* ow = obuf + row * S;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      float2 u = v[k];
+      if (k > 0 && h > 0) u = cmul(u, ldtw[r1k_tw(16 * h, k)]);  // W64^(h k) = W1024^(16 h k)
+      // h ^ 2: a = u_h0 +- u_(h0 + 2) (lanes with h & 2 hold the difference)
+      float2 r;
+      r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0x4E, 0xF, 0xF, true));
+      r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0x4E, 0xF, 0xF, true));
+      float2 a = make_float2(fmaf(sg1, u.x, r.x), fmaf(sg1, u.y, r.y));
+      // lanes h0 = 1 take W4^(s0) = (-i)^(h >> 1) before the h ^ 1 swap
+      if ((h & 1) && (h & 2)) a = make_float2(a.y, -a.x);
+      r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.x), 0xB1, 0xF, 0xF, true));
+      r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.y), 0xB1, 0xF, 0xF, true));
+      float2 xo = make_float2(fmaf(sg2, a.x, r.x), fmaf(sg2, a.y, r.y));
+      if (k == 0 && dc && k1b == 0 && h == 0) xo = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
+      ow[(k1b + 16 * k + 256 * s_out) ^ (4 * s_out)] = xo;
+    }
+    __syncthreads();
+    // thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows (chirps cb + 32 q): the Doppler transform's first step,
+    // Y[k1] = W256^(cb k1) DFT8_q, here in registers (K2 starts from the 32-point step)
+    float2 y0[8], y1[8];
+    const int pos = (2 * lt) ^ (4 * ((lt >> 7) & 3));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * S + pos);
+      y0[q] = make_float2(ab.x, ab.y);
+      y1[q] = make_float2(ab.z, ab.w);
+    }
+    Dft<8>::run(y0);
+    Dft<8>::run(y1);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float2 wk = tw[4 * cb * k];  // W256^(cb k) = W1024^(4 cb k), 4 cb k <= 868 (workgroup-uniform)
+      y0[k] = cmul(y0[k], wk);
+      y1[k] = cmul(y1[k], wk);
+    }
+    float f0[16], f1[16];
+    unsigned m0 = 0u, m1 = 0u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      f0[2 * q] = y0[q].x;
+      f0[2 * q + 1] = y0[q].y;
+      f1[2 * q] = y1[q].x;
+      f1[2 * q + 1] = y1[q].y;
+      m0 = max(m0, max(__float_as_uint(y0[q].x) & 0x7FFFFFFFu, __float_as_uint(y0[q].y) & 0x7FFFFFFFu));
+      m1 = max(m1, max(__float_as_uint(y1[q].x) & 0x7FFFFFFFu, __float_as_uint(y1[q].y) & 0x7FFFFFFFu));
+    }
+    const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+    uint4 w0[3], w1[3];
+    pk_pack16(f0, e0, w0);
+    pk_pack16(f1, e1, w1);
+    const size_t tile = (size_t)fa * ncb + cb;
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile1k) + lt;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane1k / 16)), __builtin_bit_cast(float4, w0[jj]));
+      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane1k / 16)), __builtin_bit_cast(float4, w1[jj]));
+    }
+    if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
+    __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
+  };
+  if constexpr (DYN) {
+    long t = lo + (blockIdx.x >> 3), tn = t + gx;
+    float2 nx[16];
+    if (t < hi) load(nx, t);
+    while (t < hi) {
+      body(nx, t, tn);
+      t = tn;
+      tn = *s_nn;
+    }
+    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+      atomicExch(head, 0u);
+      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+    }
+    return;
+  }
+  long t = blockIdx.x;
+  float2 nx[16];
+  if (t < ntile) load(nx, t);
+  for (; t < ntile; t += G) body(nx, t, t + G);
+}
+
+// ---------------------------------------------------------------------------------------------
 // K2: Doppler FFT.  One workgroup = KB consecutive (unshifted) range bins of one (frame, antenna):
 // reads C segments of KB contiguous complex values (KB*8 bytes each), transposes into LDS rows of
 // C points (odd stride C+1: conflict-free column writes), FFTs, and writes each shifted range row of
@@ -677,7 +861,8 @@ constexpr bool dd_reg_ok() {
 // at d (k_doppler_detect_r128).
 // SKL: the last LDS row (NR - 1 = KB + 1, the upper halo row) starts SKL float2 after its pitch position (a bank skew of
 // the caller's row writes; k_doppler_detect_r128).
-template <int C, int KB, int NT, int DBG = 0, int LD = lp_row(C) | 1, bool PADC = true, int SKL = 0>
+// HSH: columns d >= C / 2 sit HSH float2 later in their row (k_doppler_detect_r256's bank shift).
+template <int C, int KB, int NT, int DBG = 0, int LD = lp_row(C) | 1, bool PADC = true, int SKL = 0, int HSH = 0>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
                                  int* __restrict__ row_count, float* __restrict__ dbmap,
@@ -693,7 +878,7 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   if (i0 >= S) i0 -= S;
   const int rb = rh * 8;  // LDS rows rb .. rb + 9; interior rows rb + 1 .. rb + 8
   float p[10];
-  const float2* col = buf + (PADC ? lp(d) : d);
+  const float2* col = buf + (PADC ? lp(d) : d + (d >= C / 2 ? HSH : 0));
   float2* dst = rds + ((size_t)fa * S + i0 + rb) * C + j;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -996,6 +1181,145 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
   __syncthreads();
   dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL>(
       buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+}
+
+// K2 + K3 for C = 256, S = 1024 with packed `work` (the configs[4] shape; K1 = k_range_fft_r1024): the Doppler FFT
+// as 8 x 32.  K1 stored chirp class c (chirps c + 32 r, r < 8) after the radix-8 step, Y'_c[k1] = W256^(c k1) DFT8_r,
+// so thread (bin b, class c) = (tid % 16, tid / 16) loads its bin's unit (3 x 16 B) and
+//   exchange: Y' -> xi[c][(16 k1 + b) ^ 16 (c & 1)] (interior bins) and, from threads 0-63, the halo bins' values
+//   -> xh[c][(2 k1 + side) ^ (c & 15)];
+//   stage 2: lane (k1, b2, h) takes the classes c = 2 i + h: E or O = DFT16_i (registers), then the lane pair (h = 0, 1)
+//   forms X[k1 + 8 k'] = E + W32^k' O and X[k1 + 8 (k' + 16)] = E - W32^k' O by one DPP swap (as K1's radix-2 step at
+//   S = 512); 256 lanes for the 16 interior bins, 32 for the two halo bins;
+//   tile rows: X -> row b2 at the unshifted Doppler position d, columns d >= 128 one float2 later (HSH = 1) and the
+//   upper halo row 1 float2 later (SKL): every exchange and row access is bank-conflict-free except the halo rows';
+// then the register-form detection (dd_tile_compute_reg, 16 rows x 4 column waves).  X[k1 + 8 k2] = sum_c W256^(c k1)
+// W32^(c k2) sum_r x[c + 32 r] W8^(r k1): the 256-point DFT exactly.  16 bins x 256 chirps on 512 threads, 37 KiB of
+// LDS: 4 workgroups (32 waves) per CU.  DBG (development builds only): 6 no work loads, 7 loads only.
+constexpr int kR256Pitch = 258;  // tile row pitch (float2): 256 columns + the HSH shift + 1 (516 b2 = 4 b2 mod 32 dwords)
+constexpr int kR256Skew = 1;
+template <int DBG = 0>
+__global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __restrict__ work, int S_arg,
+                                                             const float2* __restrict__ tw, float2* __restrict__ rds,
+                                                             float thr_f, int i_lo, int i_hi,
+                                                             unsigned long long* __restrict__ mask,
+                                                             int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                             float* __restrict__ pk_pow,
+                                                             const unsigned char* __restrict__ wexp) {
+  constexpr int KB = 16, C = 256, S = 1024, NT = 512, NR = KB + 2, NCB = 32;
+  (void)S_arg;
+  (void)tw;
+  (void)wexp;
+  constexpr int LD = kR256Pitch, SKL = kR256Skew, HSH = 1;
+  constexpr int XPI = 8 * KB, XPH = 16;  // exchange float2 per class: interior [k1][b] (swizzled), halo [k1][side]
+  static_assert(NCB * (XPI + XPH) <= NR * LD, "exchange buffer must fit in the tile buffer");
+  extern __shared__ float2 sm[];
+  float2* buf = sm;
+  float2* xi = buf;
+  float2* xh = buf + NCB * XPI;
+  const int tid = threadIdx.x;
+  constexpr unsigned nkb = (unsigned)(S / KB);
+  const unsigned tile = (unsigned)xcd_tile(blockIdx.x, gridDim.x);
+  const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
+  auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3]) {
+    const uint4* src = reinterpret_cast<const uint4*>(wb + (tile0 + cls) * kPkTile1k +
+                                                      (size_t)(3 * (k & 1)) * kPkPlane1k) + (k >> 1);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      if constexpr (DBG == 6)
+        w[jj] = make_uint4(0x4B4000u + tid, 0x5Au * jj, 0x4B40u + k, 0x12345u);
+      else
+        w[jj] = src[jj * (kPkPlane1k / 16)];
+    }
+  };
+  const int b = tid % KB, cls = tid / KB;
+  const bool halo = tid < 2 * NCB;  // threads 0-63: (side, class) = (tid / 32, tid % 32)
+  const int hside = tid >> 5, hcls = tid & 31;
+  const int k0 = (int)(tile % nkb) * KB;
+  const unsigned fa = tile / nkb;
+  const size_t tile0 = (size_t)fa * NCB;
+  uint4 wi[3], wh[3] = {};
+  unit(tile0, k0 + b, cls, wi);
+  if (halo) {
+    int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
+    kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+    unit(tile0, kk, hcls, wh);
+  }
+  if constexpr (DBG == 7) {
+    if (__uint_as_float(wi[0].x ^ wh[1].y) == 1.2345e30f) rds[tid] = make_float2((float)wi[1].z, 0.f);
+    return;
+  }
+  {
+    float f[16];
+    pk_unpack16(wi, f);
+    float2* d = xi + cls * XPI;
+    const int sw = 16 * (cls & 1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[(16 * k + b) ^ sw] = make_float2(f[2 * k], f[2 * k + 1]);
+  }
+  if (halo) {
+    float f[16];
+    pk_unpack16(wh, f);
+    float2* d = xh + hcls * XPH;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[(2 * k + hside) ^ (hcls & 15)] = make_float2(f[2 * k], f[2 * k + 1]);
+  }
+  __syncthreads();
+  // stage 2: DFT32 over the classes as two DFT16 (c = 2 i + h) and one radix-2 step across the lane pair
+  const bool s2 = tid < 8 * KB * 2 + 32;
+  const bool hs = tid >= 8 * KB * 2;  // threads 256-287: the halo rows
+  const int u = tid - 8 * KB * 2;
+  const int hh = tid & 1;
+  const int k1 = hs ? (u >> 2) : (tid >> 5);
+  const int side = (u >> 1) & 1;
+  const int bi = (tid >> 1) & 15;
+  const int b2 = hs ? (side ? NR - 1 : 0) : bi + 1;
+  float2 x[16] = {};
+  if (s2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 2 * i + hh;
+      x[i] = hs ? xh[c * XPH + ((2 * k1 + side) ^ (c & 15))] : xi[c * XPI + ((16 * k1 + bi) ^ (16 * hh))];
+    }
+    Dft<16>::run(x);
+  }
+  __syncthreads();  // exchange reads done: the tile rows alias it (each output is written as it forms)
+  const float sg = hh ? -1.f : 1.f;
+  float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0) + k1 + (C / 2 + HSH) * hh;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float2 uu = hh ? cmul(x[k], w32(k)) : x[k];
+    float2 r;
+    r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.x), 0xB1, 0xF, 0xF, true));
+    r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.y), 0xB1, 0xF, 0xF, true));
+    if (s2) rw[8 * k] = make_float2(fmaf(sg, uu.x, r.x), fmaf(sg, uu.y, r.y));
+  }
+  __syncthreads();
+  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL, HSH>(
+      buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+}
+
+static hipError_t launch_k2d_r256(hipStream_t st, const float2* work, int F, int A, int S, float2* rds, double thr_p,
+                                  int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
+                                  float* pk_pow, int* pk_group, const unsigned char* wexp) {
+  constexpr int C = 256, KB = 16, NT = 512;
+  static_assert(dd_reg_ok<C, KB, NT>(), "register tile body shape");
+  if (S != 1024) return hipErrorInvalidValue;  // the kernel's tile math is compiled for S = 1024
+  const long ntile = (long)F * A * (S / KB);
+  const size_t lds = sizeof(float2) * (size_t)(KB + 2) * kR256Pitch + (size_t)KB * (C / 64) * 16;
+  auto kern = k_doppler_detect_r256<>;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
+    const int v = atoi(e);
+    if (v == 6) kern = k_doppler_detect_r256<6>;
+    if (v == 7) kern = k_doppler_detect_r256<7>;
+    if (v == 8) kern = k_doppler_detect_r256<8>;
+  }
+#endif
+  *pk_group = KB;
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, nullptr, rds, threshold_as_float(thr_p),
+                     i_lo, i_hi, mask, row_count, dbmap, pk_pow, wexp);
+  return hipGetLastError();
 }
 
 template <int C, int KB>
@@ -1343,6 +1667,10 @@ static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, i
     if (wexp)
       return launch_k2d_r128(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group, wexp);
   }
+  if constexpr (C == 256) {
+    if (wexp)
+      return launch_k2d_r256(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group, wexp);
+  }
   constexpr int K0 = rows_for(C);
   constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
   if (dd_kb(C, S) == K1)
@@ -1352,9 +1680,38 @@ static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, i
                               wexp);
 }
 
+// K1 at S = 1024 on packed work (work_packed_supported): k_range_fft_r1024, one tile per (frame, antenna, class).
+static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
+                                  const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+  if (C != 256) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 256
+  const long ntile = (long)F * A * 32;
+  auto kern = k_range_fft_r1024<true>;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
+    const int v = atoi(e);
+    if (v == 2) kern = k_range_fft_r1024<true, 2>;
+    if (v == 3) kern = k_range_fft_r1024<true, 3>;
+  }
+#endif
+  const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR1kThreads);
+  int slot = 0;
+  if (nblk >= 8) {
+    static std::atomic<int> next_slot{0};
+    slot = next_slot.fetch_add(1) % kRfSlots;
+  } else {
+    kern = k_range_fft_r1024<false>;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR1kThreads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
+                     work, slot, wexp);
+  return hipGetLastError();
+}
+
 template <int S>
 static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
                             const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+  if constexpr (S == 1024) {
+    if (wexp) return launch_k1_r1024(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp);
+  }
   constexpr int CB = rows_for(S);
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
     // 8 chirp rows per tile at S = 512: 16 rows (78 KiB LDS) is faster alone (1.53 vs 1.63 ms per 1000 cfg2 frames)
@@ -1510,14 +1867,16 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
 #define RSL_FFT_SIZES(X) \
   X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048) X(4096) X(25) X(50) X(100) X(200) X(400) X(800) X(1600)
 
-// Packed `work` between K1 and K2 (pk_pack16): the K1 tile holds one bin pair per thread (S = 512) and the K2 tile
-// one (bin, 8-chirp block) per thread (C = 128, KB = 16).  Development builds: RSL_WORK_C64=1 keeps c64 rows (A/B).
+// Packed `work` between K1 and K2 (pk_pack16): the K1 tile holds one bin pair per thread and the K2 tile one (bin,
+// chirp class) per thread, at the two shapes with register-form kernels: S = 512, C = 128 (k_range_fft_r512,
+// k_doppler_detect_r128) and S = 1024, C = 256 (k_range_fft_r1024, k_doppler_detect_r256).  Development builds:
+// RSL_WORK_C64=1 keeps c64 rows (A/B).
 bool work_packed_supported(int C, int S) {
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_WORK_C64"))
     if (atoi(e) != 0) return false;
 #endif
-  return S == 512 && C == 128 && doppler_detect_supported(C, S) && dd_kb(C, S) == 16;
+  return ((S == 512 && C == 128) || (S == 1024 && C == 256)) && doppler_detect_supported(C, S);
 }
 
 bool doppler_detect_supported(int C, int S) {

@@ -16,6 +16,7 @@ SHAPES = {  # name: (F, A, C, T_c)  -> K1 tiles = F * A * ceil(C / 8) at S = 512
     'ragged': (3, 3, 24, 51.2e-6),       # 27 tiles over 8 XCDs (3 or 4 each); 9 per frame
     'cfg1': (5, 8, 64, 25.6e-6),         # S = 256
     'cfg2': (40, 8, 128, 51.2e-6),       # 5120 tiles: 6.7 per resident workgroup
+    'cfg5': (6, 16, 256, 102.4e-6),      # S = 1024, packed: k_range_fft_r1024, 32 class tiles per (frame, antenna)
 }
 
 
@@ -50,10 +51,10 @@ def test_scheduling_invariance(ctx, name):
     ref = _run(ctx, ch, cube)
     assert ref[1].abs().amax().item() > 0
     what = ('work', 'rds', 'mask', 'row_count', 'peak_pow')
-    # packed `work` (S = 512, C = 128) holds 3 MiB of tiles per frame from the buffer start, so a frame's c64-sized
-    # slice (4 MiB per frame) is laid out differently in a one-frame launch: compare the outputs there, the whole buffer
+    # packed `work` (S = 512, C = 128 and S = 1024, C = 256) holds 6 B per value of tiles from the buffer start, so a
+    # frame's c64-sized slice is laid out differently in a one-frame launch: compare the outputs there, the whole buffer
     # on repeated launches
-    packed = (S, C) == (512, 128)
+    packed = (S, C) in ((512, 128), (1024, 256))
     for f in range(F):  # one launch per frame: other grids, other tile -> workgroup maps
         got = _run(ctx, ch, cube, slice(f, f + 1))
         for a, b, w in zip(ref, got, what):

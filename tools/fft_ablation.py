@@ -1,4 +1,4 @@
-"""K1 / K2 ablations on one cfg2 batch, c64 and packed `work` (development library, RSL_LIBRARY=librsl_dev.so):
+"""K1 / K2 ablations on one cfg2 batch (CFG=cfg5: one configs[4]-shape batch of 100 frames), c64 and packed `work` (development library, RSL_LIBRARY=librsl_dev.so):
 the standalone time of each kernel with one part removed (results are wrong in the variants; only times matter).
   RSL_RF_DBG: 1 no FFT, 2 no cube loads, 3 loads + LDS staging only
   RSL_DD_DBG: 1 no FFT, 4 no peak-power stores, 5 no mask stores, 6 no work loads, 7 loads + LDS staging only,
@@ -14,11 +14,12 @@ import torch  # noqa: E402
 import rsl  # noqa: E402
 from bench import make_cubes  # noqa: E402
 
-F = int(os.environ.get('F', '2000'))
+A, C, TC, F0 = {'cfg2': (8, 128, 51.2e-6, 2000), 'cfg5': (16, 256, 102.4e-6, 100)}[os.environ.get('CFG', 'cfg2')]
+F = int(os.environ.get('F', str(F0)))
 ctx = rsl.get_context(0)
-cfg = rsl.ChainConfig(num_antennas=8, num_chirps=128, chirp_duration=51.2e-6)
+cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)
 ch = rsl.RadarChain(cfg, F, ctx)
-cube = make_cubes(ctx, 1, F, 8, 128, 51.2e-6, 0)[0]
+cube = make_cubes(ctx, 1, F, A, C, TC, 0)[0]
 
 
 def run():

@@ -39,6 +39,14 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab3_*.log ;;
     ddctr) OUT=gpurun_out/${TAG}_ddctr run ddctr 400 bash tools/dd_counters.sh ;;
+    cfg5ab)  # configs[4] shape: packed register-form K1 / K2 (product) vs the c64 LDS kernels (dev library, RSL_WORK_C64=1)
+      for r in 1 2; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_C64=1 run cfg5ab_old$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
+        run cfg5ab_new$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_cfg5ab_*.log ;;
+    cfg5abl) CFG=cfg5 C64=0 RF_LIST=0,2,3 DD_LIST=0,6,7,8 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run cfg5abl 200 python -u tools/fft_ablation.py ;;
+    cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
     fused) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fused 240 python -u tools/front_fused_check.py ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
