@@ -145,7 +145,8 @@ int rsl_steer_table_build(const double* steer_c128, int G, int M, float* host_ou
  *     steer_tab = device copy of the rsl_steer_table_build output (its fp64 section feeds the exact fp64 re-scan of
  *     the cells whose top-2 gap in the f16 hi/lo or f32 scan is inside that scan's error bound, and of MUSIC's
  *     near-degenerate cells, so out_idx is the fp64 argmax of each cell's own signature; keys within 1e-13 relative
- *     count as ties and the lower index wins, as np.argmax); steer_c128 (device fp64 [G][M][2], nullable) is no
+ *     count as ties and the lower index wins, as np.argmax.  The scans' bounds are relative to the cell's best value,
+ *     so this exactness is established statistically, not by a worst-case bound); steer_c128 (device fp64 [G][M][2], nullable) is no
  *     longer read by rsl_doa / rsl_doa_extras and is kept for ABI compatibility.
  *     method = RSL_METHOD_* | RSL_DOA_TOEPLITZ (optional; with out_spec it applies to the RSL_DOA_SPEC_BLOCKED layout
  *     without out_gmax, the other spectrum requests take the f32 scan).

@@ -252,7 +252,11 @@ RSL_DEV void copy_tile(double (&dst)[8], const floatx16& src) {
 // round-3 build made had gaps <= 8.6e-8).  What decides a flip is the f16 deficit of the fp64 argmax against the f16
 // maximum: <= 2.4e-7 relative in a CPU emulation of the split (M 4 / 8 / 16, two grids, 140 k cells).  1e-6 marks
 // 0.17 % of cfg2 cells (2e-6: 0.31 %), and over 142 M cfg2 cells it gave the same indices as 2e-6
-// (tools/doa_bound_study.py, gpurun_out/r4m_bound.log).
+// (tools/doa_bound_study.py, gpurun_out/r4m_bound.log).  The bound is relative and the worst case of the dropped term
+// is absolute (about 2^-22 (2M - 1) r0): for weak, flat cells whose best value is only a few r0 that worst case would
+// exceed it, so exactness here is statistical (the emulation, the 142 M-cell study and the weak two-lobe cells of
+// tests/test_gpu_doa_exact.py), not a proof.  An absolute term max(kAmbRel best, 2^-21 (2M - 1) r0) would make it
+// one, at the price of marking most noise cells (best ~ r0 to 2 r0: a bound of ~7e-6 of best at M = 8).
 constexpr float kAmbRel = 1e-6f;
 
 // Ties of the exact scan: keys within this relative distance count as equal and the lower grid index wins, as

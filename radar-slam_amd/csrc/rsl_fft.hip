@@ -7,6 +7,8 @@
 // so the kernel zeroes range bin 0 instead of reducing a mean (exact in real arithmetic).
 // conj(ref)*w is precomputed on the host in fp64 (the chirp phase reaches 2.5e7 rad) and passed as a c64 table.
 #include <atomic>
+#include <mutex>
+#include <unordered_map>
 #include <cstdlib>
 #include <type_traits>
 
@@ -27,10 +29,23 @@ namespace rsl {
 constexpr int kThreads = 256;
 
 // K1 work queues (RSL_RF_DYN): per launch slot, 8 per-XCD dequeue heads and 8 exit counters, each on its own 128-B
-// line. The last workgroup of an XCD to leave resets its pair, so a slot is clean for its next launch; the host
-// hands slots round-robin, so up to kRfSlots K1 launches may be in flight at once (on any streams).
-constexpr int kRfSlots = 8;
+// line. The last workgroup of an XCD to leave resets its pair, so a slot is clean for its next launch.  A slot belongs
+// to one stream (rf_slot): launches on one stream run in order, so no two K1 launches in flight ever share a slot, for
+// up to kRfSlots streams per process (round 4 handed slots round-robin over all launches, which let the 8-slot ring
+// wrap onto a launch still queued on another stream: ADVICE r4).
+constexpr int kRfSlots = 64;
 __device__ unsigned g_rf_q[kRfSlots][2][8][32];
+
+static int rf_slot(hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, int> slots;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = slots.find(st);
+  if (it != slots.end()) return it->second;
+  const int s = (int)(slots.size() % kRfSlots);
+  slots.emplace(st, s);
+  return s;
+}
 
 // Global accesses with an optional non-temporal hint (`nt`: streamed once, not kept in L2 / MALL).
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -644,11 +659,13 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
     Dft<16>::run(v);
     const float sg1 = (h & 2) ? -1.f : 1.f, sg2 = (h & 1) ? -1.f : 1.f;
     __syncthreads();  // xbuf reads done: obuf aliases it (the radix-4 step below writes each output as it forms)
-    float2* ow = obuf + row * S;
+    // bin k1 + 16 k + 256 s at (bin ^ 4 s) = ((k1 ^ 4 s) + 256 s) + 16 k: one base, constant offsets
+    float2* ow = obuf + row * S + ((k1b ^ (4 * s_out)) + 256 * s_out);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       float2 u = v[k];
-      if (k > 0 && h > 0) u = cmul(u, ldtw[r1k_tw(16 * h, k)]);  // W64^(h k) = W1024^(16 h k)
+      // W64^(h k) = W1024^(16 h k); unconditional (lanes h = 0 multiply by W^0 = 1: exact up to the sign of a zero)
+      if (k > 0) u = cmul(u, ldtw[r1k_tw(16 * h, k)]);
       // h ^ 2: a = u_h0 +- u_(h0 + 2) (lanes with h & 2 hold the difference)
       float2 r;
       r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0x4E, 0xF, 0xF, true));
@@ -660,7 +677,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
       r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.y), 0xB1, 0xF, 0xF, true));
       float2 xo = make_float2(fmaf(sg2, a.x, r.x), fmaf(sg2, a.y, r.y));
       if (k == 0 && dc && k1b == 0 && h == 0) xo = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
-      ow[(k1b + 16 * k + 256 * s_out) ^ (4 * s_out)] = xo;
+      ow[16 * k] = xo;
     }
     __syncthreads();
     // thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows (chirps cb + 32 q): the Doppler transform's first step,
@@ -1081,7 +1098,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 // class c (chirps c + 16 r, r < 8) as one packed tile after the first radix-8 step, Y'_c[k1] = W128^(c k1) DFT8_r
 // x[c + 16 r] (k_range_fft_r512), so thread (bin b, class c) = (tid % 16, tid / 16) loads the 8 values of its bin
 // (3 x 16 B) and
-//   exchange: Y' -> xi[c][k1][b] (interior bins, 128 float2 per class) and, from threads 0-31, the two halo bins'
+//   exchange: Y' -> xi[c][k1][b] (interior bins, 128 float2 per class) and, from every 8th thread, the two halo bins'
 //   values -> xh[c][k1][side] (17 float2 per class);
 //   stage 2: thread t < 128 = (k1 = t / 16, b = t % 16) reads xi[c][k1][b], threads 128-143 = (k1, side) read
 //   xh[c][k1][side], for c < 16 (consecutive per instruction); X[k1 + 8 k2] = DFT16_c (registers), written to tile row
@@ -1132,8 +1149,10 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
     }
   };
   const int b = tid % KB, cls = tid / KB;
-  const bool halo = tid < 2 * NCB;  // threads 0-31: (side, class) = (tid / 16, tid % 16)
-  const int hside = tid >> 4, hcls = tid & 15;
+  // the 32 halo units spread over the 4 waves (every 8th thread) instead of all on wave 0: (side, class) = (h / 16,
+  // h % 16), h = tid / 8
+  const bool halo = (tid & 7) == 0;
+  const int hside = tid >> 7, hcls = (tid >> 3) & 15;
   const int k0 = (int)(tile % nkb) * KB;
   const unsigned fa = tile / nkb;
   const size_t tile0 = (size_t)fa * NCB;
@@ -1186,8 +1205,8 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
 // K2 + K3 for C = 256, S = 1024 with packed `work` (the configs[4] shape; K1 = k_range_fft_r1024): the Doppler FFT
 // as 8 x 32.  K1 stored chirp class c (chirps c + 32 r, r < 8) after the radix-8 step, Y'_c[k1] = W256^(c k1) DFT8_r,
 // so thread (bin b, class c) = (tid % 16, tid / 16) loads its bin's unit (3 x 16 B) and
-//   exchange: Y' -> xi[c][(16 k1 + b) ^ 16 (c & 1)] (interior bins) and, from threads 0-63, the halo bins' values
-//   -> xh[c][(2 k1 + side) ^ (c & 15)];
+//   exchange: Y' -> xi[c][(16 k1 + b) ^ 16 (c & 1)] (interior bins) and, from every 8th thread, the halo bins'
+//   values -> xh[c][(2 k1 + side) ^ (c & 15)];
 //   stage 2: lane (k1, b2, h) takes the classes c = 2 i + h: E or O = DFT16_i (registers), then the lane pair (h = 0, 1)
 //   forms X[k1 + 8 k'] = E + W32^k' O and X[k1 + 8 (k' + 16)] = E - W32^k' O by one DPP swap (as K1's radix-2 step at
 //   S = 512); 256 lanes for the 16 interior bins, 32 for the two halo bins;
@@ -1233,8 +1252,10 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
     }
   };
   const int b = tid % KB, cls = tid / KB;
-  const bool halo = tid < 2 * NCB;  // threads 0-63: (side, class) = (tid / 32, tid % 32)
-  const int hside = tid >> 5, hcls = tid & 31;
+  // the 64 halo units spread over the 8 waves (every 8th thread) instead of all on wave 0: (side, class) = (h / 32,
+  // h % 32), h = tid / 8
+  const bool halo = (tid & 7) == 0;
+  const int hside = tid >> 8, hcls = (tid >> 3) & 31;
   const int k0 = (int)(tile % nkb) * KB;
   const unsigned fa = tile / nkb;
   const size_t tile0 = (size_t)fa * NCB;
@@ -1275,14 +1296,19 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
   const int bi = (tid >> 1) & 15;
   const int b2 = hs ? (side ? NR - 1 : 0) : bi + 1;
   float2 x[16] = {};
-  if (s2) {
+  // wave-uniform branches: waves 0-3 read interior classes, lanes 0-31 of wave 4 the halo ones
+  if (tid < 8 * KB * 2) {
+    const float2* src = xi + hh * XPI + ((16 * k1 + bi) ^ (16 * hh));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = src[2 * i * XPI];
+  } else if (s2) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = 2 * i + hh;
-      x[i] = hs ? xh[c * XPH + ((2 * k1 + side) ^ (c & 15))] : xi[c * XPI + ((16 * k1 + bi) ^ (16 * hh))];
+      x[i] = xh[c * XPH + ((2 * k1 + side) ^ (c & 15))];
     }
-    Dft<16>::run(x);
   }
+  if (s2) Dft<16>::run(x);
   __syncthreads();  // exchange reads done: the tile rows alias it (each output is written as it forms)
   const float sg = hh ? -1.f : 1.f;
   float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0) + k1 + (C / 2 + HSH) * hh;
@@ -1693,14 +1719,11 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
     if (v == 3) kern = k_range_fft_r1024<true, 3>;
   }
 #endif
+  // ntile >= 32 (A >= 1, 32 classes) and every CU holds two workgroups: the grid always spans the 8 XCDs, so the
+  // per-XCD dequeue always applies (no static-walk instance)
   const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR1kThreads);
-  int slot = 0;
-  if (nblk >= 8) {
-    static std::atomic<int> next_slot{0};
-    slot = next_slot.fetch_add(1) % kRfSlots;
-  } else {
-    kern = k_range_fft_r1024<false>;
-  }
+  if (nblk < 8) return hipErrorInvalidValue;
+  const int slot = rf_slot(st);
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR1kThreads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
                      work, slot, wexp);
   return hipGetLastError();
@@ -1755,8 +1778,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
 #endif
     int slot = 0;
     if (nblk >= 8) {  // the per-XCD dequeue needs a workgroup on every XCD
-      static std::atomic<int> next_slot{0};
-      slot = next_slot.fetch_add(1) % kRfSlots;
+      slot = rf_slot(st);
     } else {
       kern = k_range_fft_p<S, CB, false>;
       if constexpr (S == 512 && CB == 8) {

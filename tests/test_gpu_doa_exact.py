@@ -6,7 +6,10 @@ tie).  The signatures are built to land on the cases the scans' rounding cannot 
   - the +-90 degree pair (identical steering vectors at d = lambda / 2: an exact tie, lower index);
   - signatures peaked halfway (in phase) between two grid points, inside a 32-point tile and across a tile boundary
     (a near-tie the f16 / f32 scans cannot order);
-  - random signatures.
+  - random signatures, and weak noise-like two-lobe cells (two near-equal lobes far apart under noise of their size).
+The scans' ambiguity bounds are relative to the cell's best value (rsl_doa_toep.hip kAmbRel): the exactness they give
+is established by the CPU emulation of the split scan and the 142 M-cell GPU study, not by a
+worst-case bound, and these cases are its regression test.
 Paths: the fused Toeplitz scan with ESPRIT / phase (rsl_doa_extras), the Toeplitz argmax (rsl_doa fast), the f32
 [Re; Im] scan (rsl_doa fast=False) and the f32 scan with the spectrum (k_doa_scan)."""
 import numpy as np
@@ -43,6 +46,15 @@ def _signatures(A, grid, rs):
         for amp in (0.0, 1e-3):
             sig.append(np.exp(1j * mid * m) + amp * (rs.randn(A) + 1j * rs.randn(A)))
     sig += list(rs.randn(200, A) + 1j * rs.randn(200, A))
+    # weak, noise-like two-lobe cells: two equal or nearly equal lobes at grid points far apart under noise
+    # of the same size, so the cell's best value is only a few times r0 and its top two sit in different tiles: the
+    # ambiguity bound is relative to the best value, and these cells are where an absolute scan error would show
+    for k in range(240):
+        g1, g2 = rs.choice(361, 2, replace=False)
+        a2 = 1.0 + (0.0, 1e-7, 1e-6, 1e-5)[k % 4]
+        noise = (0.3, 1.0)[(k // 4) % 2]
+        sig.append(np.exp(1j * phi[g1] * m) + a2 * np.exp(1j * phi[g2] * m)
+                   + noise * (rs.randn(A) + 1j * rs.randn(A)))
     return np.array(sig).astype(np.complex64)
 
 

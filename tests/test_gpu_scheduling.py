@@ -2,8 +2,8 @@
 walk of smaller grids must not change a single bit of the range spectra, RDS, peak masks or peak powers.
 
 Each case runs the same device cubes as one batch and as one launch per frame (a different grid, a different tile ->
-workgroup assignment and different dequeue heads), then 20 more batch launches, so every queue slot (8, round-robin)
-has been reused after its self-reset: grids below 8 workgroups (the static walk), tile counts that do not divide over
+workgroup assignment and different dequeue heads), then 20 more batch launches, so the stream's queue slot has been
+reused after its self-reset: grids below 8 workgroups (the static walk), tile counts that do not divide over
 the 8 XCDs, and batches far larger than the resident grid.
 """
 import pytest
@@ -65,3 +65,35 @@ def test_scheduling_invariance(ctx, name):
         got = _run(ctx, ch, cube)
         for a, b, w in zip(ref, got, what):
             assert torch.equal(_bits(a), _bits(b)), f'{name}: {w} differs on launch {rep}'
+
+
+def test_concurrent_streams(ctx):
+    """K1 launches in flight on several streams at once: each stream owns its dequeue slot (rsl_fft.hip
+    rf_slot), so chains of two shapes on three streams, 8 launches each, all enqueued before any completes, give the
+    serial results bit for bit."""
+    import rsl
+    shapes = [(6, 8, 128, 51.2e-6), (6, 8, 128, 51.2e-6), (2, 16, 256, 102.4e-6)]
+    chains, cubes, refs = [], [], []
+    g = torch.Generator(device='cuda').manual_seed(11)
+    for F, A, C, Tc in shapes:
+        ch = rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, ctx)
+        S = ch.rds.shape[2]
+        cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
+                             torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
+        chains.append(ch)
+        cubes.append(cube)
+        refs.append(_run(ctx, ch, cube))
+    streams = [torch.cuda.Stream() for _ in shapes]
+    outs = [[] for _ in shapes]
+    torch.cuda.synchronize()
+    for rep in range(8):
+        for k, (ch, cube, st) in enumerate(zip(chains, cubes, streams)):
+            with torch.cuda.stream(st):
+                ctx.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                               row_count=ch.row_count, peak_pow=ch.peak_pow, dc_removal=True)
+                outs[k].append([t.clone() for t in (ch.rds, ch.mask, ch.row_count)])
+    torch.cuda.synchronize()
+    for k in range(len(shapes)):
+        for rep, got in enumerate(outs[k]):
+            for a, b, w in zip((refs[k][1], refs[k][2], refs[k][3]), got, ('rds', 'mask', 'row_count')):
+                assert torch.equal(_bits(a), _bits(b)), f'stream {k}: {w} differs on launch {rep}'

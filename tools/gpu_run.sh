@@ -19,6 +19,7 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     tests) run tests 560 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread ;;
+    tsel) run tsel 400 python -u -m pytest tests/test_gpu_dbmap.py tests/test_gpu_doa_exact.py tests/test_gpu_chain.py tests/test_gpu_scheduling.py tests/test_gpu_pipelined.py -x -q --timeout 150 --timeout-method thread ;;
     testsall) run testsall 600 python -u -m pytest tests -m gpu -q --maxfail 12 --timeout 150 --timeout-method thread ;;
     doavar) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run doavar 300 python -u tools/doa_var_time.py 0
       RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run doavar_ab 200 python -u tools/doa_var_time.py 0 ;;
@@ -39,6 +40,7 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab3_*.log ;;
     ddctr) OUT=gpurun_out/${TAG}_ddctr run ddctr 400 bash tools/dd_counters.sh ;;
+    ddctr5) CFG=cfg5 OUT=gpurun_out/${TAG}_ddctr5 run ddctr5 400 bash tools/dd_counters.sh ;;
     cfg5ab)  # configs[4] shape: packed register-form K1 / K2 (product) vs the c64 LDS kernels (dev library, RSL_WORK_C64=1)
       for r in 1 2; do
         RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_WORK_C64=1 run cfg5ab_old$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
@@ -46,6 +48,12 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_cfg5ab_*.log ;;
     cfg5abl) CFG=cfg5 C64=0 RF_LIST=0,2,3 DD_LIST=0,6,7,8 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run cfg5abl 200 python -u tools/fft_ablation.py ;;
+    ab5)  # configs[4] shape: product vs radar-slam_amd/lib/librsl_ab.so (tools/build_ab.sh), 2 rounds
+      for r in 1 2; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run ab5_old$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
+        run ab5_new$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_ab5_*.log ;;
     cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
     fused) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fused 240 python -u tools/front_fused_check.py ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
