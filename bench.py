@@ -426,6 +426,8 @@ def kernel_bytes_k1k2(A, C, S, F):
     c64 `work` at other shapes (k_range_fft_p / k_doppler_detect): 2 A C S 8 B per frame each."""
     if (C, S) in ((128, 512), (256, 1024)):  # packed (cfg2; cfg5: k_range_fft_r1024 / k_doppler_detect_r256, the same)
         return {'range_fft': A * C * S * 14.0 * F, 'doppler_fft': A * C * S * (6.0 * 18 / 16 + 8) * F}
+    if (C, S) == (64, 256):  # packed, 32-bin K2 tiles (k_doppler_detect_r64)
+        return {'range_fft': A * C * S * 14.0 * F, 'doppler_fft': A * C * S * (6.0 * 34 / 32 + 8) * F}
     return {'range_fft': 2 * A * C * S * 8 * F, 'doppler_fft': 2 * A * C * S * 8 * F}
 
 
@@ -598,7 +600,8 @@ def chain_rooflines(r, A, C, S, F, config):
     #     evaluated as three f16 MFMA products for fp32 accuracy (hi/lo split) -> 3 * 2 * (2M - 1) flops
     src_std = ks if ks else kt
     fft_names = {(128, 512): {'range_fft': 'k_range_fft_r512', 'doppler_fft': 'k_doppler_detect_r128'},
-                 (256, 1024): {'range_fft': 'k_range_fft_r1024', 'doppler_fft': 'k_doppler_detect_r256'}}.get(
+                 (256, 1024): {'range_fft': 'k_range_fft_r1024', 'doppler_fft': 'k_doppler_detect_r256'},
+                 (64, 256): {'range_fft': 'k_range_fft_r256', 'doppler_fft': 'k_doppler_detect_r64'}}.get(
         (C, S), {'range_fft': 'k_range_fft_p', 'doppler_fft': 'k_doppler_detect'})
     per_std = lambda name: src_std[name][0] / max(src_std[name][1], 1)
     flops = 3 * 2 * (2 * A - 1) * ncl * G

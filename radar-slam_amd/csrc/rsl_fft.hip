@@ -745,6 +745,150 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
 }
 
 // ---------------------------------------------------------------------------------------------
+// K1 for S = 256 with packed `work` (the cfg1 / configs[0] shape: C = 64): the same chirp-class tiles on
+// 128 threads.  A tile is chirp class c of one (frame, antenna), the 8 chirps c + 8 q (q < 8, c < 8); K2
+// (k_doppler_detect_r64) does the 8-point step over the classes.  16 lanes per chirp row:
+//   x[n], n = j + 16 m (j, m < 16): lane j of row q loads x[j + 16 m] (8-B loads, 128-B runs), x conj(ref) w;
+//   stage 1: V[j][k1] = DFT16_m, times W256^(j k1) (LDS, XOR-swizzled);
+//   exchange: V -> xbuf[q][k1][j ^ k1 ^ (q & 1)] (both rows of a 32-lane read group cover the 64 banks once);
+//   stage 2: lane (q, k1) takes the 16 j: X[k1 + 16 k2] = DFT16_j, no cross-lane step;
+//   output: -> obuf[q][bin] (aliasing xbuf), then thread p reads bins 2p, 2p + 1 of the 8 rows (16-B reads), takes
+//   W64^(c k1) DFT8_q and stores both bins packed (planes of 128 pairs x 16 B).
+// LDS 20 KiB: 8 workgroups (16 waves) per CU.
+constexpr int kR256Threads = 128;
+constexpr int kPkPlane256 = 8 * 256;        // bytes per plane of one S = 256 tile (128 pairs x 16 B)
+constexpr int kPkTile256 = 6 * kPkPlane256;
+RSL_DEV int r256_tw(int j, int k) { return j * 16 + (k ^ j); }  // W256^(j k) in ldtw
+
+template <int DBG = 0>
+__global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* __restrict__ cube, int A, int Ct, int c0,
+                                                                 int C, long ntile, const float2* __restrict__ table,
+                                                                 const float2* __restrict__ tw, int dc,
+                                                                 float2* __restrict__ work, int slot,
+                                                                 unsigned char* __restrict__ wexp) {
+  constexpr int S = 256, NT = kR256Threads, ncb = 8;  // C = 64 wherever this kernel runs (work_packed_supported)
+  (void)wexp;
+  (void)C;
+  (void)A;
+  __shared__ float2 ldtab[S];
+  __shared__ float2 ldtw[16 * 16];
+  __shared__ float2 xbuf[8 * S];  // stage exchange; aliased by the output buffer
+  __shared__ long s_nn;
+  float2* obuf = xbuf;
+  const int tid = threadIdx.x;
+  const long G = gridDim.x;
+  for (int k = tid; k < S; k += NT) ldtab[k] = table[k];
+  for (int k = tid; k < 16 * 16; k += NT) {
+    const int jj = k >> 4, kk = k & 15;
+    ldtw[r256_tw(jj, kk)] = tw[jj * kk];  // W256^(j k1), j k1 <= 225
+  }
+  auto load = [&](float2(&nx)[16], long t) {
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 4, j = lt & 15;
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 8 * row) * S + j;  // chirp class cb, row q = row
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if constexpr (DBG == 2)
+        nx[m] = make_float2((float)tid, (float)m);
+      else
+        nx[m] = ld8<true>(src + 16 * m);
+    }
+  };
+  const int xcd = blockIdx.x & 7;
+  const long gx = (G - xcd + 7) / 8;
+  const long lo = xcd * ntile / 8, hi = (xcd + 1) * ntile / 8;
+  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  __syncthreads();
+  auto body = [&](float2(&nx)[16], long t, long tn) {
+    unsigned claim = 0;
+    if (tid == 0) claim = atomicAdd(head, 1u);
+    const int cb = (int)(t % ncb);
+    const long fa = t / ncb;
+    int lt = tid;  // laundered per tile: keeps the tile-invariant table reads inside the tile loop
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 4, j = lt & 15, k1 = lt & 15;
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 16 * m]);
+    load(nx, tn < hi ? tn : t);  // in flight during this tile's transforms and stores
+    Dft<16>::run(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[r256_tw(j, k)]);
+    float2* xw = xbuf + row * S;
+    const int rsw = j ^ (row & 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xw[k * 16 + (rsw ^ k)] = v[k];
+    __syncthreads();
+    const float2* xr = xbuf + row * S + k1 * 16;
+    const int rk = k1 ^ (row & 1);
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = xr[jj ^ rk];
+    Dft<16>::run(v);
+    if (dc && k1 == 0) v[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
+    __syncthreads();  // xbuf reads done: obuf aliases it
+    float2* ow = obuf + row * S + k1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ow[16 * k] = v[k];
+    __syncthreads();
+    // thread lt holds bins 2 lt, 2 lt + 1 of the 8 rows (chirps cb + 8 q): Y[k1] = W64^(cb k1) DFT8_q
+    float2 y0[8], y1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * S + 2 * lt);
+      y0[q] = make_float2(ab.x, ab.y);
+      y1[q] = make_float2(ab.z, ab.w);
+    }
+    Dft<8>::run(y0);
+    Dft<8>::run(y1);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float2 wk = tw[4 * cb * k];  // W64^(cb k) = W256^(4 cb k), 4 cb k <= 196 (workgroup-uniform)
+      y0[k] = cmul(y0[k], wk);
+      y1[k] = cmul(y1[k], wk);
+    }
+    float f0[16], f1[16];
+    unsigned m0 = 0u, m1 = 0u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      f0[2 * q] = y0[q].x;
+      f0[2 * q + 1] = y0[q].y;
+      f1[2 * q] = y1[q].x;
+      f1[2 * q + 1] = y1[q].y;
+      m0 = max(m0, max(__float_as_uint(y0[q].x) & 0x7FFFFFFFu, __float_as_uint(y0[q].y) & 0x7FFFFFFFu));
+      m1 = max(m1, max(__float_as_uint(y1[q].x) & 0x7FFFFFFFu, __float_as_uint(y1[q].y) & 0x7FFFFFFFu));
+    }
+    const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+    uint4 w0[3], w1[3];
+    pk_pack16(f0, e0, w0);
+    pk_pack16(f1, e1, w1);
+    const size_t tile = (size_t)fa * ncb + cb;
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(work) + tile * kPkTile256) + lt;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane256 / 16)), __builtin_bit_cast(float4, w0[jj]));
+      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane256 / 16)), __builtin_bit_cast(float4, w1[jj]));
+    }
+    if (tid == 0) s_nn = lo + 2 * gx + (long)claim;
+    __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
+  };
+  long t = lo + (blockIdx.x >> 3), tn = t + gx;
+  float2 nx[16];
+  if (t < hi) load(nx, t);
+  while (t < hi) {
+    body(nx, t, tn);
+    t = tn;
+    tn = s_nn;
+  }
+  if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+    atomicExch(head, 0u);
+    atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // K2: Doppler FFT.  One workgroup = KB consecutive (unshifted) range bins of one (frame, antenna):
 // reads C segments of KB contiguous complex values (KB*8 bytes each), transposes into LDS rows of
 // C points (odd stride C+1: conflict-free column writes), FFTs, and writes each shifted range row of
@@ -1325,6 +1469,126 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
       buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
 }
 
+// K2 + K3 for C = 64, S = 256 with packed `work` (the cfg1 shape; K1 = k_range_fft_r256): the Doppler FFT as 8 x 8.
+// K1 stored chirp class c (chirps c + 8 r, r < 8) after the radix-8 step, Y'_c[k1] = W64^(c k1) DFT8_r, so thread
+// (bin b, class c) = (tid % 32, tid / 32) loads its bin's unit (3 x 16 B) and decodes it into xi[c][k1][b] (every 16th
+// thread a halo unit into xh[c][k1][side]); lane (k1, b) then takes X[k1 + 8 k2] = DFT8_c (registers) for its interior
+// bin and threads 0-15 the halo bins' transforms, each written to its tile row (rows C + 1 apart: conflict-free); the
+// register-form detection (one column wave x 4 row quarters) follows.  32 bins x 64 chirps on 256 threads, 18 KiB LDS.
+template <int DBG = 0>
+__global__ __launch_bounds__(256) void k_doppler_detect_r64(const float2* __restrict__ work, int S_arg,
+                                                            const float2* __restrict__ tw, float2* __restrict__ rds,
+                                                            float thr_f, int i_lo, int i_hi,
+                                                            unsigned long long* __restrict__ mask,
+                                                            int* __restrict__ row_count, float* __restrict__ dbmap,
+                                                            float* __restrict__ pk_pow,
+                                                            const unsigned char* __restrict__ wexp) {
+  constexpr int KB = 32, C = 64, S = 256, NT = 256, NR = KB + 2, NCB = 8;
+  (void)S_arg;
+  (void)tw;
+  (void)wexp;
+  constexpr int LD = C + 1;
+  constexpr int XPI = 8 * KB, XPH = 16;  // exchange float2 per class: interior [k1][b], halo [k1][side]
+  static_assert(NCB * (XPI + XPH) <= NR * LD, "exchange buffer must fit in the tile buffer");
+  extern __shared__ float2 sm[];
+  float2* buf = sm;
+  float2* xi = buf;
+  float2* xh = buf + NCB * XPI;
+  const int tid = threadIdx.x;
+  constexpr unsigned nkb = (unsigned)(S / KB);
+  const unsigned tile = (unsigned)xcd_tile(blockIdx.x, gridDim.x);
+  const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
+  auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3]) {
+    const uint4* src = reinterpret_cast<const uint4*>(wb + (tile0 + cls) * kPkTile256 +
+                                                      (size_t)(3 * (k & 1)) * kPkPlane256) + (k >> 1);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      if constexpr (DBG == 6)
+        w[jj] = make_uint4(0x4B4000u + tid, 0x5Au * jj, 0x4B40u + k, 0x12345u);
+      else
+        w[jj] = src[jj * (kPkPlane256 / 16)];
+    }
+  };
+  const int b = tid % KB, cls = tid / KB;
+  const bool halo = (tid & 15) == 0;  // 16 halo units, one per 16 threads: (side, class) = (h / 8, h % 8), h = tid / 16
+  const int hside = tid >> 7, hcls = (tid >> 4) & 7;
+  const int k0 = (int)(tile % nkb) * KB;
+  const unsigned fa = tile / nkb;
+  const size_t tile0 = (size_t)fa * NCB;
+  uint4 wi[3], wh[3] = {};
+  unit(tile0, k0 + b, cls, wi);
+  if (halo) {
+    int kk = hside ? k0 + KB : k0 - 1;  // periodic: 'reflect' is applied in the detect stage
+    kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+    unit(tile0, kk, hcls, wh);
+  }
+  {
+    float f[16];
+    pk_unpack16(wi, f);
+    float2* d = xi + cls * XPI + b;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k * KB] = make_float2(f[2 * k], f[2 * k + 1]);
+  }
+  if (halo) {
+    float f[16];
+    pk_unpack16(wh, f);
+    float2* d = xh + hcls * XPH + hside;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[2 * k] = make_float2(f[2 * k], f[2 * k + 1]);
+  }
+  __syncthreads();
+  // stage 2: DFT8 over the classes; lane (k1, b) = (tid / 32, tid % 32) for the interior bins, threads 0-15 also
+  // (k1, side) = (tid / 2, tid % 2) for the halo bins
+  const int k1 = tid / KB;
+  float2 x[8], y[8] = {};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) x[c] = xi[c * XPI + k1 * KB + b];
+  Dft<8>::run(x);
+  const bool hs = tid < 16;
+  const int hk1 = tid >> 1, hsd = tid & 1;
+  if (hs) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) y[c] = xh[c * XPH + 2 * hk1 + hsd];
+    Dft<8>::run(y);
+  }
+  __syncthreads();  // exchange reads done: the tile rows alias it
+  {
+    float2* rw = buf + (b + 1) * LD + k1;
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) rw[8 * k2] = x[k2];
+  }
+  if (hs) {
+    float2* rw = buf + (hsd ? NR - 1 : 0) * LD + hk1;
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) rw[8 * k2] = y[k2];
+  }
+  __syncthreads();
+  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false>(
+      buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+}
+
+static hipError_t launch_k2d_r64(hipStream_t st, const float2* work, int F, int A, int S, float2* rds, double thr_p,
+                                 int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
+                                 float* pk_pow, int* pk_group, const unsigned char* wexp) {
+  constexpr int C = 64, KB = 32, NT = 256;
+  static_assert(dd_reg_ok<C, KB, NT>(), "register tile body shape");
+  if (S != 256) return hipErrorInvalidValue;  // the kernel's tile math is compiled for S = 256
+  const long ntile = (long)F * A * (S / KB);
+  const size_t lds = sizeof(float2) * (size_t)(KB + 2) * (C + 1) + (size_t)KB * (C / 64) * 16;
+  auto kern = k_doppler_detect_r64<>;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
+    const int v = atoi(e);
+    if (v == 6) kern = k_doppler_detect_r64<6>;
+    if (v == 8) kern = k_doppler_detect_r64<8>;
+  }
+#endif
+  *pk_group = KB;
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntile), dim3(NT), lds, st, work, S, nullptr, rds, threshold_as_float(thr_p),
+                     i_lo, i_hi, mask, row_count, dbmap, pk_pow, wexp);
+  return hipGetLastError();
+}
+
 static hipError_t launch_k2d_r256(hipStream_t st, const float2* work, int F, int A, int S, float2* rds, double thr_p,
                                   int i_lo, int i_hi, unsigned long long* mask, int* row_count, float* dbmap,
                                   float* pk_pow, int* pk_group, const unsigned char* wexp) {
@@ -1697,6 +1961,10 @@ static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, i
     if (wexp)
       return launch_k2d_r256(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group, wexp);
   }
+  if constexpr (C == 64) {
+    if (wexp)
+      return launch_k2d_r64(st, work, F, A, S, rds, thr_p, i_lo, i_hi, mask, row_count, dbmap, pk_pow, pk_group, wexp);
+  }
   constexpr int K0 = rows_for(C);
   constexpr int K1 = (2048 / C) < 1 ? 1 : (2048 / C) > K0 ? K0 : (2048 / C);
   if (dd_kb(C, S) == K1)
@@ -1729,11 +1997,33 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
   return hipGetLastError();
 }
 
+// K1 at S = 256 on packed work (work_packed_supported): k_range_fft_r256, one tile per (frame, antenna, class).
+static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
+                                 const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+  if (C != 64) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 64
+  const long ntile = (long)F * A * 8;
+  auto kern = k_range_fft_r256<>;
+#ifdef RSL_DEV_KNOBS
+  if (const char* e = getenv("RSL_RF_DBG"))  // ablation (development builds only; results are wrong)
+    if (atoi(e) == 2) kern = k_range_fft_r256<2>;
+#endif
+  // the per-XCD dequeue needs a workgroup on every XCD: tiny batches (F A < 1) do not occur (ntile >= 8)
+  const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR256Threads);
+  if (nblk < 8) return hipErrorInvalidValue;
+  const int slot = rf_slot(st);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR256Threads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
+                     work, slot, wexp);
+  return hipGetLastError();
+}
+
 template <int S>
 static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
                             const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
   if constexpr (S == 1024) {
     if (wexp) return launch_k1_r1024(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp);
+  }
+  if constexpr (S == 256) {
+    if (wexp) return launch_k1_r256(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp);
   }
   constexpr int CB = rows_for(S);
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
@@ -1890,15 +2180,17 @@ hipError_t launch_doppler_dft(hipStream_t st, const float2* work, int F, int A, 
   X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048) X(4096) X(25) X(50) X(100) X(200) X(400) X(800) X(1600)
 
 // Packed `work` between K1 and K2 (pk_pack16): the K1 tile holds one bin pair per thread and the K2 tile one (bin,
-// chirp class) per thread, at the two shapes with register-form kernels: S = 512, C = 128 (k_range_fft_r512,
-// k_doppler_detect_r128) and S = 1024, C = 256 (k_range_fft_r1024, k_doppler_detect_r256).  Development builds:
+// chirp class) per thread, at the three shapes with register-form kernels: S = 512, C = 128 (k_range_fft_r512,
+// k_doppler_detect_r128), S = 1024, C = 256 (k_range_fft_r1024, k_doppler_detect_r256) and S = 256, C = 64
+// (k_range_fft_r256, k_doppler_detect_r64).  Development builds:
 // RSL_WORK_C64=1 keeps c64 rows (A/B).
 bool work_packed_supported(int C, int S) {
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_WORK_C64"))
     if (atoi(e) != 0) return false;
 #endif
-  return ((S == 512 && C == 128) || (S == 1024 && C == 256)) && doppler_detect_supported(C, S);
+  return ((S == 512 && C == 128) || (S == 1024 && C == 256) || (S == 256 && C == 64)) &&
+         doppler_detect_supported(C, S);
 }
 
 bool doppler_detect_supported(int C, int S) {

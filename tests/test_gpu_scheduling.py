@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = {  # name: (F, A, C, T_c)  -> K1 tiles = F * A * ceil(C / 8) at S = 512
     'below8': (3, 1, 16, 51.2e-6),       # 2 tiles per frame: the per-frame grids are below 8 (static walk)
     'ragged': (3, 3, 24, 51.2e-6),       # 27 tiles over 8 XCDs (3 or 4 each); 9 per frame
-    'cfg1': (5, 8, 64, 25.6e-6),         # S = 256
+    'cfg1': (5, 8, 64, 25.6e-6),         # S = 256, packed: k_range_fft_r256, 8 class tiles per (frame, antenna)
     'cfg2': (40, 8, 128, 51.2e-6),       # 5120 tiles: 6.7 per resident workgroup
     'cfg5': (6, 16, 256, 102.4e-6),      # S = 1024, packed: k_range_fft_r1024, 32 class tiles per (frame, antenna)
 }
@@ -51,10 +51,10 @@ def test_scheduling_invariance(ctx, name):
     ref = _run(ctx, ch, cube)
     assert ref[1].abs().amax().item() > 0
     what = ('work', 'rds', 'mask', 'row_count', 'peak_pow')
-    # packed `work` (S = 512, C = 128 and S = 1024, C = 256) holds 6 B per value of tiles from the buffer start, so a
-    # frame's c64-sized slice is laid out differently in a one-frame launch: compare the outputs there, the whole buffer
-    # on repeated launches
-    packed = (S, C) in ((512, 128), (1024, 256))
+    # packed `work` (S = 512, C = 128; S = 1024, C = 256; S = 256, C = 64) holds 6 B per value of tiles from the buffer
+    # start, so a frame's c64-sized slice is laid out differently in a one-frame launch: compare the outputs there, the
+    # whole buffer on repeated launches
+    packed = (S, C) in ((512, 128), (1024, 256), (256, 64))
     for f in range(F):  # one launch per frame: other grids, other tile -> workgroup maps
         got = _run(ctx, ch, cube, slice(f, f + 1))
         for a, b, w in zip(ref, got, what):
@@ -97,3 +97,24 @@ def test_concurrent_streams(ctx):
         for rep, got in enumerate(outs[k]):
             for a, b, w in zip((refs[k][1], refs[k][2], refs[k][3]), got, ('rds', 'mask', 'row_count')):
                 assert torch.equal(_bits(a), _bits(b)), f'stream {k}: {w} differs on launch {rep}'
+
+
+@pytest.mark.parametrize('name', ['cfg1', 'cfg2', 'cfg5'])
+def test_chirp_window_packed(ctx, name):
+    """A chirp window (chirp0 > 0 inside a longer cube) on the packed paths: K1 reads its class rows at the window's
+    offset; the outputs equal those of the window copied out as its own contiguous cube."""
+    import rsl
+    F, A, C, Tc = {'cfg1': (2, 8, 64, 25.6e-6), 'cfg2': (2, 8, 128, 51.2e-6), 'cfg5': (1, 16, 256, 102.4e-6)}[name]
+    ch = rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, ctx)
+    S = ch.rds.shape[2]
+    c0, Ct = 5, C + 9
+    g = torch.Generator(device='cuda').manual_seed(3)
+    big = torch.complex(torch.randn(F, A, Ct, S, device='cuda', generator=g),
+                        torch.randn(F, A, Ct, S, device='cuda', generator=g)) * 0.1
+    ref = _run(ctx, ch, big[:, :, c0:c0 + C].contiguous())
+    bufs = [t.zero_() for t in (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow)]
+    ctx.rds_detect(big, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                   row_count=ch.row_count, peak_pow=ch.peak_pow, chirp0=c0, num_chirps=C, dc_removal=True)
+    torch.cuda.synchronize()
+    for a, b, w in zip(ref, bufs, ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
+        assert torch.equal(_bits(a), _bits(b)), f'{name}: {w} differs for the chirp window'
