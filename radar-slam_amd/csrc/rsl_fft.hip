@@ -402,7 +402,7 @@ RSL_DEV float2 w32(int k) {                // exp(-2 pi i k / 32), k < 16
   return make_float2(c[k], c[(k + 8) & 15] * (k < 8 ? 1.f : -1.f));  // -sin(2 pi k / 32)
 }
 
-template <bool DYN, int DBG = 0, bool NTW = true>
+template <bool DYN, int DBG = 0, bool NTW = true, bool SWZ = false>
 __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                               int C, long ntile, const float2* __restrict__ table,
                                                               const float2* __restrict__ tw, int dc,
@@ -410,21 +410,24 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
                                                               unsigned char* __restrict__ wexp) {
   constexpr int S = 512, CB = 8;
   (void)wexp;  // the exponents travel inside the packed units (pk_pack16)
+  // SWZ: XOR-swizzled LDS instead of padded pitches (exchange [row][k1][j ^ 2 k1], twiddles [j][k ^ (j / 2)], output
+  // [row][bin ^ 8 (bin / 256)]), the tile hand-off word in a twiddle slot no lane reads: 40 KiB, 4 workgroups per CU
+  constexpr int XP = SWZ ? 32 : kR512Pitch, TWP = SWZ ? 16 : kR512TwPitch, OBP = SWZ ? S : kR512Obuf;
   __shared__ float2 ldtab[S];
-  __shared__ float2 ldtw[32 * kR512TwPitch];
-  __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // stage exchange; aliased by the output buffer
-  static_assert(CB * kR512Obuf <= CB * 16 * kR512Pitch, "output buffer must fit in the exchange buffer");
+  __shared__ float2 ldtw[32 * TWP];
+  __shared__ float2 xbuf[CB * 16 * XP];  // stage exchange; aliased by the output buffer
+  static_assert(CB * OBP <= CB * 16 * XP, "output buffer must fit in the exchange buffer");
   float2* obuf = xbuf;
+  auto twi = [](int jj, int kk) { return SWZ ? jj * 16 + (kk ^ ((jj >> 1) & 15)) : jj * kR512TwPitch + kk; };
   const int tid = threadIdx.x;
-  const int row = tid >> 5, j = tid & 31;
-  const int k1b = (tid >> 1) & 15, h = tid & 1;
+  const int row = tid >> 5, j = tid & 31;  // the load's lane map (the tile body derives its own)
   constexpr int ncb = 128 / CB;  // C = 128 wherever this kernel runs (work_packed_supported): tile index math by shifts
   (void)C;
   const long G = gridDim.x;
   for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
   for (int k = tid; k < 32 * 16; k += kThreads) {
     const int jj = k >> 4, kk = k & 15;
-    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
+    if (!SWZ || kk) ldtw[twi(jj, kk)] = tw[jj * kk];  // W512^(j k1), j k1 <= 465 (SWZ: k1 = 0 is never read)
   }
   auto load = [&](float2(&nx)[16], long t) {
     const int cb = (int)(t % ncb);
@@ -438,7 +441,8 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
         nx[m] = ld8<true>(src + 32 * m);
     }
   };
-  __shared__ long s_nn;
+  __shared__ long s_nn_own[SWZ ? 1 : 1];
+  long* s_nn = SWZ ? reinterpret_cast<long*>(&ldtw[twi(0, 0)]) : &s_nn_own[0];
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
@@ -449,6 +453,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     if (DYN && tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
+    int lt = tid;  // SWZ: laundered per tile (keeps the tile-invariant LDS reads inside the tile loop)
+    if constexpr (SWZ) asm volatile("" : "+v"(lt));
+    const int row = lt >> 5, j = lt & 31;
+    const int k1b = (lt >> 1) & 15, h = lt & 1;
     float2 v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 32 * m]);
@@ -457,22 +465,22 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     load(nx, tn < hi ? tn : t);
     if constexpr (DBG == 3) {
       if (v[0].x == 1.2345e30f) work[tid] = v[1];
-      if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
+      if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
       __syncthreads();
       return;
     }
     // stage 1: DFT16 over m, twiddle W512^(j k1)
     Dft<16>::run(v);
 #pragma unroll
-    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[j * kR512TwPitch + k]);
-    float2* xw = xbuf + row * 16 * kR512Pitch + j;
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[twi(j, k)]);
+    float2* xw = xbuf + row * 16 * XP;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) xw[k * kR512Pitch] = v[k];
+    for (int k = 0; k < 16; ++k) xw[k * XP + (SWZ ? (j ^ (2 * k)) : j)] = v[k];
     __syncthreads();
     // stage 2: DFT16 over i of V'[2 i + h][k1], then the radix-2 combine across the lane pair (h = 0, 1)
-    const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
+    const float2* xr = xbuf + (row * 16 + k1b) * XP;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
+    for (int i = 0; i < 16; ++i) v[i] = xr[SWZ ? (2 * (i ^ k1b) + h) : (2 * i + h)];
     Dft<16>::run(v);
     // lane h = 0 holds E[k], lane h = 1 holds O[k]: u = E[k] or W32^k O[k], swapped with the partner lane by DPP;
     // bin k1 + 16 k = E + W O on h = 0 (u + recv), bin k1 + 16 (k + 16) = E - W O on h = 1 (recv - u): one packed
@@ -489,17 +497,18 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     }
     if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
     __syncthreads();  // xbuf reads done: obuf aliases it
-    float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;  // bin k1 + 16 k + 256 h at position bin + 8 h
+    // bin k1 + 16 k + 256 h at position bin + 8 h (SWZ: bin ^ 8 h)
+    float2* ow = obuf + row * OBP + (SWZ ? ((k1b ^ (8 * h)) + 256 * h) : (k1b + 264 * h));
 #pragma unroll
     for (int k = 0; k < 16; ++k) ow[16 * k] = xo[k];
     __syncthreads();
     // thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows (chirps cb + 16 q): the Doppler transform's first step,
     // Y[k1] = W128^(cb k1) DFT8_q, here in registers (K2 starts from the 16-point step)
     float2 y0[8], y1[8];
-    const int pos = 2 * tid + (tid >= 128 ? 8 : 0);
+    const int pos = SWZ ? ((2 * tid) ^ (tid >= 128 ? 8 : 0)) : 2 * tid + (tid >= 128 ? 8 : 0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * kR512Obuf + pos);
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * OBP + pos);
       y0[q] = make_float2(ab.x, ab.y);
       y1[q] = make_float2(ab.z, ab.w);
     }
@@ -534,7 +543,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
       st16<NTW>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
       st16<NTW>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
     }
-    if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
+    if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
     __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
   };
   if constexpr (DYN) {
@@ -544,7 +553,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     while (t < hi) {
       body(nx, t, tn);
       t = tn;
-      tn = s_nn;
+      tn = *s_nn;
     }
     if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
       atomicExch(head, 0u);
@@ -1947,6 +1956,258 @@ hipError_t launch_front_fused(hipStream_t st, const float2* cube, int F, int A, 
                      row_count, pk_pow);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Front half as a PAIR of concurrent persistent kernels on two streams (development study, RSL_FRONT_PAIR=1): the L2
+// ring hand-off of k_front_r512, but each role with its own register / LDS budget and occupancy: k_front_k1p (the K1
+// body, 2 workgroups per CU) produces slab b's 16 class tiles into ring slot b % kFrR of its XCD, k_front_k2p (the K2
+// body, 3 workgroups per CU, 19 KiB each) consumes them.  Both claim their XCD's items in slab order from their own
+// queue heads; a K2 item waits for its slab's 16 done counts, a K1 item's stores wait until the slot's previous slab
+// has been read by its 32 K2 tiles.  Deadlock-free while each kernel has a resident workgroup on every XCD (the grids
+// leave room for each other on every CU: 2 x 43 + 3 x 19 KiB of LDS), and every wait is bounded as in k_front_r512.
+struct FpQueue {  // one 128-B line per counter
+  unsigned head1[8][32];
+  unsigned head2[8][32];
+  unsigned done[8][kFrR][32];
+  unsigned cons[8][kFrR][32];
+  unsigned err[32];
+};
+
+__global__ __launch_bounds__(kThreads) void k_front_k1p(const float2* __restrict__ cube, int Ct, int c0, int nslab,
+                                                         const float2* __restrict__ table,
+                                                         const float2* __restrict__ tw, int dc,
+                                                         unsigned char* __restrict__ ring, FpQueue* __restrict__ q) {
+  constexpr int S = 512, CB = 8;
+  __shared__ float2 ldtab[S];
+  __shared__ float2 ldtw[32 * kR512TwPitch];
+  __shared__ float2 xbuf[CB * 16 * kR512Pitch];
+  __shared__ int s_nn;
+  float2* obuf = xbuf;
+  const int tid = threadIdx.x;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const int x = (int)(xcc & 7u);
+  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
+  const int total = 16 * nx;
+  for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
+  for (int k = tid; k < 32 * 16; k += kThreads) {
+    const int jj = k >> 4, kk = k & 15;
+    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];
+  }
+  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
+  auto load = [&](float2(&nx_)[16], int t) {
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 5, j = lt & 31;
+    const float2* src = cube + ((size_t)(s0 + t / 16) * Ct + c0 + (t % 16) + 16 * row) * S + j;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) nx_[m] = ld8<true>(src + 32 * m);
+  };
+  if (tid == 0) s_nn = (int)atomicAdd(&q->head1[x][0], 1u);
+  __syncthreads();
+  int t = s_nn;
+  __syncthreads();
+  float2 nxv[16];
+  if (t < total) load(nxv, t);
+  while (t < total) {
+    unsigned claim = 0;
+    if (tid == 0) claim = atomicAdd(&q->head1[x][0], 1u);
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int row = lt >> 5, j = lt & 31;
+    const int k1b = (lt >> 1) & 15, h = lt & 1;
+    const int b = t / 16, cb = t % 16, slot = b % kFrR;
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = cmul(nxv[m], ldtab[j + 32 * m]);
+    // the next item is known once the claim issued above has returned: its cube loads start after stage 2
+    Dft<16>::run(v);
+#pragma unroll
+    for (int kk = 1; kk < 16; ++kk) v[kk] = cmul(v[kk], ldtw[j * kR512TwPitch + kk]);
+    float2* xw = xbuf + row * 16 * kR512Pitch + j;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) xw[kk * kR512Pitch] = v[kk];
+    __syncthreads();
+    const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
+    Dft<16>::run(v);
+    float2 xo[16];
+    const rsl_f2v sgn = h ? (rsl_f2v){-1.f, -1.f} : (rsl_f2v){1.f, 1.f};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const float2 u = h ? cmul(v[kk], w32(kk)) : v[kk];
+      float2 recv;
+      recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0xB1, 0xF, 0xF, true));
+      recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0xB1, 0xF, 0xF, true));
+      xo[kk] = cf(__builtin_elementwise_fma(sgn, cv(u), cv(recv)));
+    }
+    if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);
+    if (tid == 0) s_nn = (int)claim;
+    __syncthreads();
+    const int tn = s_nn;
+    float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) ow[16 * kk] = xo[kk];
+    __syncthreads();
+    if (tn < total) load(nxv, tn);  // in flight during the Doppler step, the packing and the ring wait
+    float2 y0[8], y1[8];
+    const int pos = 2 * lt + (lt >= 128 ? 8 : 0);
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + qq * kR512Obuf + pos);
+      y0[qq] = make_float2(ab.x, ab.y);
+      y1[qq] = make_float2(ab.z, ab.w);
+    }
+    Dft<8>::run(y0);
+    Dft<8>::run(y1);
+#pragma unroll
+    for (int kk = 1; kk < 8; ++kk) {
+      const float2 wk = tw[4 * cb * kk];
+      y0[kk] = cmul(y0[kk], wk);
+      y1[kk] = cmul(y1[kk], wk);
+    }
+    float f0[16], f1[16];
+    unsigned m0 = 0u, m1 = 0u;
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      f0[2 * qq] = y0[qq].x;
+      f0[2 * qq + 1] = y0[qq].y;
+      f1[2 * qq] = y1[qq].x;
+      f1[2 * qq + 1] = y1[qq].y;
+      m0 = max(m0, max(__float_as_uint(y0[qq].x) & 0x7FFFFFFFu, __float_as_uint(y0[qq].y) & 0x7FFFFFFFu));
+      m1 = max(m1, max(__float_as_uint(y1[qq].x) & 0x7FFFFFFFu, __float_as_uint(y1[qq].y) & 0x7FFFFFFFu));
+    }
+    const int e0 = pk_exp(m0), e1 = pk_exp(m1);
+    uint4 w0[3], w1[3];
+    pk_pack16(f0, e0, w0);
+    pk_pack16(f1, e1, w1);
+    fr_wait(&q->cons[x][slot][0], 32u * (unsigned)(b / kFrR), &q->err[0]);  // slab b - kFrR has left the slot
+    uint4* dst = reinterpret_cast<uint4*>(xring + ((size_t)slot * 16 + cb) * kPkTile) + lt;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
+      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&q->done[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = tn;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_front_k2p(int nslab, unsigned char* __restrict__ ring, FpQueue* __restrict__ q,
+                                                   float2* __restrict__ rds, float thr_f, int i_lo, int i_hi,
+                                                   unsigned long long* __restrict__ mask, int* __restrict__ row_count,
+                                                   float* __restrict__ pk_pow) {
+  constexpr int S = 512, C = 128, KB = 16, NR = KB + 2, NCB = 16, LD = kR128Pitch, SKL = kR128Skew, XPI = 8 * KB;
+  constexpr int XPH = 17;
+  extern __shared__ float2 sm[];
+  float2* buf = sm;
+  float2* xi = buf;
+  float2* xh = buf + NCB * XPI;
+  __shared__ int s_item;
+  const int tid = threadIdx.x;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const int x = (int)(xcc & 7u);
+  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
+  const int total = 32 * nx;
+  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
+  for (;;) {
+    if (tid == 0) s_item = (int)atomicAdd(&q->head2[x][0], 1u);
+    __syncthreads();
+    const int k = s_item;
+    __syncthreads();
+    if (k >= total) break;
+    const int bb = k / 32, slot = bb % kFrR;
+    fr_wait(&q->done[x][slot][0], 16u * (unsigned)(bb / kFrR + 1), &q->err[0]);
+    const int k0 = (k % 32) * KB;
+    const unsigned fa = (unsigned)(s0 + bb);
+    const unsigned char* tiles = xring + (size_t)slot * 16 * kPkTile;
+    auto unit = [&](int kk, int cls, uint4(&w)[3]) {
+      const uint4* src = reinterpret_cast<const uint4*>(tiles + (size_t)cls * kPkTile +
+                                                        (size_t)(3 * (kk & 1)) * kPkPlane) + (kk >> 1);
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj)
+        w[jj] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + jj * (kPkPlane / 16))));
+    };
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    const int bq = lt % KB, cls = lt / KB;
+    const bool halo = (lt & 7) == 0;
+    const int hside = lt >> 7, hcls = (lt >> 3) & 15;
+    uint4 wi[3], wh[3] = {};
+    unit(k0 + bq, cls, wi);
+    if (halo) {
+      int kk = hside ? k0 + KB : k0 - 1;
+      kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
+      unit(kk, hcls, wh);
+    }
+    auto stage1 = [&](const uint4(&w)[3], float2* d, int st) {
+      float f[16];
+      pk_unpack16(w, f);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) d[kk * st] = make_float2(f[2 * kk], f[2 * kk + 1]);
+    };
+    stage1(wi, xi + cls * XPI + bq, KB);
+    if (halo) stage1(wh, xh + hcls * XPH + hside, 2);
+    __syncthreads();  // every ring load of this tile has returned
+    if (tid == 0) __hip_atomic_fetch_add(&q->cons[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool s2 = lt < 8 * NR;
+    const bool hs = lt >= 8 * KB;
+    const int k1 = hs ? (lt - 8 * KB) >> 1 : lt / KB;
+    const int b2 = hs ? ((lt & 1) ? NR - 1 : 0) : (lt % KB) + 1;
+    float2 xv[16] = {};
+    if (s2) {
+      const float2* src = hs ? xh + 2 * k1 + (lt & 1) : xi + lt;
+      const int cs = hs ? XPH : XPI;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) xv[c] = src[c * cs];
+      Dft<16>::run(xv);
+    }
+    __syncthreads();
+    if (s2) {
+      float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0);
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) rw[k1 + 8 * k2] = xv[k2];
+    }
+    __syncthreads();
+    dd_tile_compute_reg<C, KB, 256, 0, LD, false, SKL>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds,
+                                                       thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow, lt);
+    __syncthreads();
+  }
+}
+
+hipError_t launch_front_pair(hipStream_t st, hipStream_t st2, hipEvent_t ev0, hipEvent_t ev1, const float2* cube,
+                             int F, int A, int Ct, int c0, int C, int S, const float2* table, const float2* tw_S, int dc,
+                             float2* work, size_t work_bytes, float2* rds, double thr_p, int i_lo, int i_hi,
+                             unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow, int* pk_group) {
+  if (S != 512 || C != 128 || dbmap || !st2 || !ev0 || !ev1) return hipErrorNotSupported;
+  const size_t need = kFrRingBytes + sizeof(FpQueue);
+  if (work_bytes < need || (long)F * A < 8) return hipErrorNotSupported;
+  unsigned char* ring = reinterpret_cast<unsigned char*>(work);
+  FpQueue* q = reinterpret_cast<FpQueue*>(ring + kFrRingBytes);
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  int n1 = 2, n2 = 3;
+  if (const char* e = getenv("RSL_FRONT_PAIR_WG")) sscanf(e, "%d,%d", &n1, &n2);
+  const size_t lds2 = sizeof(float2) * 18 * kR128Pitch + 16 * 2 * 16;
+  if (hipError_t e = hipMemsetAsync(q, 0, sizeof(FpQueue), st)) return e;
+  if (hipError_t e = hipEventRecord(ev0, st)) return e;
+  if (hipError_t e = hipStreamWaitEvent(st2, ev0, 0)) return e;
+  *pk_group = 16;
+  const float thr_f = threshold_as_float(thr_p);
+  hipLaunchKernelGGL(k_front_k2p, dim3((unsigned)(n2 * ncu)), dim3(256), lds2, st2, F * A, ring, q, rds, thr_f, i_lo,
+                     i_hi, mask, row_count, pk_pow);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(k_front_k1p, dim3((unsigned)(n1 * ncu)), dim3(kThreads), 0, st, cube, Ct, c0, F * A, table, tw_S,
+                     dc, ring, q);
+  if (hipError_t e = hipGetLastError()) return e;
+  if (hipError_t e = hipEventRecord(ev1, st2)) return e;
+  return hipStreamWaitEvent(st, ev1, 0);
+}
 #endif  // RSL_DEV_KNOBS
 
 template <int C>
@@ -2044,6 +2305,10 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     if constexpr (S == 512 && CB == 8) {  // RSL_WORK_TEMPORAL=1: the packed `work` stored without the nt hint (MALL study)
       if (const char* e = getenv("RSL_WORK_TEMPORAL"))
         if (wexp && atoi(e) == 1) kern = k_range_fft_r512<true, 0, false>;
+    }
+    if constexpr (S == 512 && CB == 8) {  // RSL_R512_SWZ=1: XOR-swizzled LDS, 40 KiB, 4 workgroups per CU
+      if (const char* e = getenv("RSL_R512_SWZ"))
+        if (wexp && atoi(e) == 1) kern = k_range_fft_r512<true, 0, true, true>;
     }
     if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
       const int v = atoi(e);
