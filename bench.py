@@ -34,7 +34,7 @@ PROFILE = os.path.join(ROOT, 'profiles', 'r5g_pmc.json')  # rocprofv3 FETCH_SIZE
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
-CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r5h_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
+CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r5j_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
 STANDALONE_RUNS = 6  # unpipelined chain runs after the timed region (kernel_ms_standalone, fft_stage_standalone)
 TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
                   ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')

@@ -29,10 +29,6 @@ struct rsl_context {
   // the live timeline of the launches since the reset, every stream's launches on one device clock
   hipEvent_t t0 = nullptr;
   std::vector<std::pair<double, double>> span[RSL_K_COUNT];
-#ifdef RSL_DEV_KNOBS
-  hipStream_t st2 = nullptr;  // development study RSL_FRONT_PAIR: the second stream of the concurrent K1 / K2 pair
-  hipEvent_t pev[2] = {nullptr, nullptr};
-#endif
 };
 
 namespace {
@@ -149,11 +145,6 @@ int rsl_destroy(rsl_handle h) {
     hipEventDestroy(p.second);
   }
   if (h->t0) hipEventDestroy(h->t0);
-#ifdef RSL_DEV_KNOBS
-  if (h->st2) hipStreamDestroy(h->st2);
-  for (auto e : h->pev)
-    if (e) hipEventDestroy(e);
-#endif
   delete h;
   return RSL_OK;
 }
@@ -266,37 +257,6 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   // the first 3/4 of the c64-sized work buffer the caller provides; wexp is the launchers' packed-path switch)
   unsigned char* wexp =
       rsl::work_packed_supported(C, S) ? (unsigned char*)work + (size_t)F * A * C * S * 6 : nullptr;
-#ifdef RSL_DEV_KNOBS
-  if (const char* fe = getenv("RSL_FRONT_PAIR"); fe && atoi(fe) == 1 && wexp && chirp0 == 0 && C_total == C) {
-    // development study: K1 and K2 as two concurrent persistent kernels with the L2 ring (rsl_fft.hip k_front_k1p/k2p)
-    if (!h->st2) {
-      hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking);
-      hipEventCreateWithFlags(&h->pev[0], hipEventDisableTiming);
-      hipEventCreateWithFlags(&h->pev[1], hipEventDisableTiming);
-    }
-    Scope sc(h, RSL_K_RANGE_FFT);
-    e = rsl::launch_front_pair(h->stream, h->st2, h->pev[0], h->pev[1], (const float2*)cube, F, A, C_total, chirp0, C,
-                               S, (const float2*)table, tS, dc_removal, (float2*)work,
-                               (size_t)F * A * C * S * sizeof(float2), (float2*)rds, thr_power, i_lo, i_hi,
-                               (unsigned long long*)mask, (int*)row_count, (float*)db_map, (float*)peak_pow, &group);
-    if (e != hipErrorNotSupported) {
-      if (peak_pow_group) *peak_pow_group = group;
-      return hip_check(h, e, "front_pair");
-    }
-  }
-  if (const char* fe = getenv("RSL_FRONT_FUSED"); fe && atoi(fe) == 1 && wexp && chirp0 == 0 && C_total == C) {
-    // development study: K1 + K2 in one launch with the packed work in a per-XCD L2 ring (rsl_fft.hip k_front_r512)
-    Scope sc(h, RSL_K_RANGE_FFT);
-    e = rsl::launch_front_fused(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                                dc_removal, (float2*)work, (size_t)F * A * C * S * sizeof(float2), (float2*)rds,
-                                thr_power, i_lo, i_hi, (unsigned long long*)mask, (int*)row_count, (float*)db_map,
-                                (float*)peak_pow, &group);
-    if (e != hipErrorNotSupported) {
-      if (peak_pow_group) *peak_pow_group = group;
-      return hip_check(h, e, "front_fused");
-    }
-  }
-#endif
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,

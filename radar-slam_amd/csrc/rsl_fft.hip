@@ -402,7 +402,7 @@ RSL_DEV float2 w32(int k) {                // exp(-2 pi i k / 32), k < 16
   return make_float2(c[k], c[(k + 8) & 15] * (k < 8 ? 1.f : -1.f));  // -sin(2 pi k / 32)
 }
 
-template <bool DYN, int DBG = 0, bool NTW = true, bool SWZ = false>
+template <bool DYN, int DBG = 0, bool NTW = true>
 __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                               int C, long ntile, const float2* __restrict__ table,
                                                               const float2* __restrict__ tw, int dc,
@@ -410,24 +410,21 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
                                                               unsigned char* __restrict__ wexp) {
   constexpr int S = 512, CB = 8;
   (void)wexp;  // the exponents travel inside the packed units (pk_pack16)
-  // SWZ: XOR-swizzled LDS instead of padded pitches (exchange [row][k1][j ^ 2 k1], twiddles [j][k ^ (j / 2)], output
-  // [row][bin ^ 8 (bin / 256)]), the tile hand-off word in a twiddle slot no lane reads: 40 KiB, 4 workgroups per CU
-  constexpr int XP = SWZ ? 32 : kR512Pitch, TWP = SWZ ? 16 : kR512TwPitch, OBP = SWZ ? S : kR512Obuf;
   __shared__ float2 ldtab[S];
-  __shared__ float2 ldtw[32 * TWP];
-  __shared__ float2 xbuf[CB * 16 * XP];  // stage exchange; aliased by the output buffer
-  static_assert(CB * OBP <= CB * 16 * XP, "output buffer must fit in the exchange buffer");
+  __shared__ float2 ldtw[32 * kR512TwPitch];
+  __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // stage exchange; aliased by the output buffer
+  static_assert(CB * kR512Obuf <= CB * 16 * kR512Pitch, "output buffer must fit in the exchange buffer");
   float2* obuf = xbuf;
-  auto twi = [](int jj, int kk) { return SWZ ? jj * 16 + (kk ^ ((jj >> 1) & 15)) : jj * kR512TwPitch + kk; };
   const int tid = threadIdx.x;
-  const int row = tid >> 5, j = tid & 31;  // the load's lane map (the tile body derives its own)
+  const int row = tid >> 5, j = tid & 31;
+  const int k1b = (tid >> 1) & 15, h = tid & 1;
   constexpr int ncb = 128 / CB;  // C = 128 wherever this kernel runs (work_packed_supported): tile index math by shifts
   (void)C;
   const long G = gridDim.x;
   for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
   for (int k = tid; k < 32 * 16; k += kThreads) {
     const int jj = k >> 4, kk = k & 15;
-    if (!SWZ || kk) ldtw[twi(jj, kk)] = tw[jj * kk];  // W512^(j k1), j k1 <= 465 (SWZ: k1 = 0 is never read)
+    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
   }
   auto load = [&](float2(&nx)[16], long t) {
     const int cb = (int)(t % ncb);
@@ -441,8 +438,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
         nx[m] = ld8<true>(src + 32 * m);
     }
   };
-  __shared__ long s_nn_own[SWZ ? 1 : 1];
-  long* s_nn = SWZ ? reinterpret_cast<long*>(&ldtw[twi(0, 0)]) : &s_nn_own[0];
+  __shared__ long s_nn;
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
@@ -453,10 +449,6 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     if (DYN && tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
-    int lt = tid;  // SWZ: laundered per tile (keeps the tile-invariant LDS reads inside the tile loop)
-    if constexpr (SWZ) asm volatile("" : "+v"(lt));
-    const int row = lt >> 5, j = lt & 31;
-    const int k1b = (lt >> 1) & 15, h = lt & 1;
     float2 v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = cmul(nx[m], ldtab[j + 32 * m]);
@@ -465,22 +457,22 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     load(nx, tn < hi ? tn : t);
     if constexpr (DBG == 3) {
       if (v[0].x == 1.2345e30f) work[tid] = v[1];
-      if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
+      if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
       __syncthreads();
       return;
     }
     // stage 1: DFT16 over m, twiddle W512^(j k1)
     Dft<16>::run(v);
 #pragma unroll
-    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[twi(j, k)]);
-    float2* xw = xbuf + row * 16 * XP;
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], ldtw[j * kR512TwPitch + k]);
+    float2* xw = xbuf + row * 16 * kR512Pitch + j;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) xw[k * XP + (SWZ ? (j ^ (2 * k)) : j)] = v[k];
+    for (int k = 0; k < 16; ++k) xw[k * kR512Pitch] = v[k];
     __syncthreads();
     // stage 2: DFT16 over i of V'[2 i + h][k1], then the radix-2 combine across the lane pair (h = 0, 1)
-    const float2* xr = xbuf + (row * 16 + k1b) * XP;
+    const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = xr[SWZ ? (2 * (i ^ k1b) + h) : (2 * i + h)];
+    for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
     Dft<16>::run(v);
     // lane h = 0 holds E[k], lane h = 1 holds O[k]: u = E[k] or W32^k O[k], swapped with the partner lane by DPP;
     // bin k1 + 16 k = E + W O on h = 0 (u + recv), bin k1 + 16 (k + 16) = E - W O on h = 1 (recv - u): one packed
@@ -497,18 +489,17 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     }
     if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
     __syncthreads();  // xbuf reads done: obuf aliases it
-    // bin k1 + 16 k + 256 h at position bin + 8 h (SWZ: bin ^ 8 h)
-    float2* ow = obuf + row * OBP + (SWZ ? ((k1b ^ (8 * h)) + 256 * h) : (k1b + 264 * h));
+    float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;  // bin k1 + 16 k + 256 h at position bin + 8 h
 #pragma unroll
     for (int k = 0; k < 16; ++k) ow[16 * k] = xo[k];
     __syncthreads();
     // thread tid holds bins 2 tid, 2 tid + 1 of the 8 rows (chirps cb + 16 q): the Doppler transform's first step,
     // Y[k1] = W128^(cb k1) DFT8_q, here in registers (K2 starts from the 16-point step)
     float2 y0[8], y1[8];
-    const int pos = SWZ ? ((2 * tid) ^ (tid >= 128 ? 8 : 0)) : 2 * tid + (tid >= 128 ? 8 : 0);
+    const int pos = 2 * tid + (tid >= 128 ? 8 : 0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * OBP + pos);
+      const float4 ab = *reinterpret_cast<const float4*>(obuf + q * kR512Obuf + pos);
       y0[q] = make_float2(ab.x, ab.y);
       y1[q] = make_float2(ab.z, ab.w);
     }
@@ -543,7 +534,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
       st16<NTW>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
       st16<NTW>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
     }
-    if (DYN && tid == 0) *s_nn = lo + 2 * gx + (long)claim;
+    if (DYN && tid == 0) s_nn = lo + 2 * gx + (long)claim;
     __syncthreads();  // obuf is read above; the next tile's exchange writes overwrite it
   };
   if constexpr (DYN) {
@@ -553,7 +544,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     while (t < hi) {
       body(nx, t, tn);
       t = tn;
-      tn = *s_nn;
+      tn = s_nn;
     }
     if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
       atomicExch(head, 0u);
@@ -1251,7 +1242,7 @@ __global__ __launch_bounds__(NT) void k_doppler_detect(const float2* __restrict_
 // class c (chirps c + 16 r, r < 8) as one packed tile after the first radix-8 step, Y'_c[k1] = W128^(c k1) DFT8_r
 // x[c + 16 r] (k_range_fft_r512), so thread (bin b, class c) = (tid % 16, tid / 16) loads the 8 values of its bin
 // (3 x 16 B) and
-//   exchange: Y' -> xi[c][k1][b] (interior bins, 128 float2 per class) and, from every 8th thread, the two halo bins'
+//   exchange: Y' -> xi[c][k1][b] (interior bins, 128 float2 per class) and, from threads 0-31, the two halo bins'
 //   values -> xh[c][k1][side] (17 float2 per class);
 //   stage 2: thread t < 128 = (k1 = t / 16, b = t % 16) reads xi[c][k1][b], threads 128-143 = (k1, side) read
 //   xh[c][k1][side], for c < 16 (consecutive per instruction); X[k1 + 8 k2] = DFT16_c (registers), written to tile row
@@ -1302,10 +1293,8 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
     }
   };
   const int b = tid % KB, cls = tid / KB;
-  // the 32 halo units spread over the 4 waves (every 8th thread) instead of all on wave 0: (side, class) = (h / 16,
-  // h % 16), h = tid / 8
-  const bool halo = (tid & 7) == 0;
-  const int hside = tid >> 7, hcls = (tid >> 3) & 15;
+  const bool halo = tid < 2 * NCB;  // threads 0-31: (side, class) = (tid / 16, tid % 16)
+  const int hside = tid >> 4, hcls = tid & 15;
   const int k0 = (int)(tile % nkb) * KB;
   const unsigned fa = tile / nkb;
   const size_t tile0 = (size_t)fa * NCB;
@@ -1358,8 +1347,8 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
 // K2 + K3 for C = 256, S = 1024 with packed `work` (the configs[4] shape; K1 = k_range_fft_r1024): the Doppler FFT
 // as 8 x 32.  K1 stored chirp class c (chirps c + 32 r, r < 8) after the radix-8 step, Y'_c[k1] = W256^(c k1) DFT8_r,
 // so thread (bin b, class c) = (tid % 16, tid / 16) loads its bin's unit (3 x 16 B) and
-//   exchange: Y' -> xi[c][(16 k1 + b) ^ 16 (c & 1)] (interior bins) and, from every 8th thread, the halo bins'
-//   values -> xh[c][(2 k1 + side) ^ (c & 15)];
+//   exchange: Y' -> xi[c][(16 k1 + b) ^ 16 (c & 1)] (interior bins) and, from threads 0-63, the halo bins' values
+//   -> xh[c][(2 k1 + side) ^ (c & 15)];
 //   stage 2: lane (k1, b2, h) takes the classes c = 2 i + h: E or O = DFT16_i (registers), then the lane pair (h = 0, 1)
 //   forms X[k1 + 8 k'] = E + W32^k' O and X[k1 + 8 (k' + 16)] = E - W32^k' O by one DPP swap (as K1's radix-2 step at
 //   S = 512); 256 lanes for the 16 interior bins, 32 for the two halo bins;
@@ -1405,10 +1394,8 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
     }
   };
   const int b = tid % KB, cls = tid / KB;
-  // the 64 halo units spread over the 8 waves (every 8th thread) instead of all on wave 0: (side, class) = (h / 32,
-  // h % 32), h = tid / 8
-  const bool halo = (tid & 7) == 0;
-  const int hside = tid >> 8, hcls = (tid >> 3) & 31;
+  const bool halo = tid < 2 * NCB;  // threads 0-63: (side, class) = (tid / 32, tid % 32)
+  const int hside = tid >> 5, hcls = tid & 31;
   const int k0 = (int)(tile % nkb) * KB;
   const unsigned fa = tile / nkb;
   const size_t tile0 = (size_t)fa * NCB;
@@ -1449,19 +1436,14 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
   const int bi = (tid >> 1) & 15;
   const int b2 = hs ? (side ? NR - 1 : 0) : bi + 1;
   float2 x[16] = {};
-  // wave-uniform branches: waves 0-3 read interior classes, lanes 0-31 of wave 4 the halo ones
-  if (tid < 8 * KB * 2) {
-    const float2* src = xi + hh * XPI + ((16 * k1 + bi) ^ (16 * hh));
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = src[2 * i * XPI];
-  } else if (s2) {
+  if (s2) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int c = 2 * i + hh;
-      x[i] = xh[c * XPH + ((2 * k1 + side) ^ (c & 15))];
+      x[i] = hs ? xh[c * XPH + ((2 * k1 + side) ^ (c & 15))] : xi[c * XPI + ((16 * k1 + bi) ^ (16 * hh))];
     }
+    Dft<16>::run(x);
   }
-  if (s2) Dft<16>::run(x);
   __syncthreads();  // exchange reads done: the tile rows alias it (each output is written as it forms)
   const float sg = hh ? -1.f : 1.f;
   float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0) + k1 + (C / 2 + HSH) * hh;
@@ -1694,521 +1676,6 @@ static hipError_t launch_k2d_r128(hipStream_t st, const float2* work, int F, int
   return hipGetLastError();
 }
 
-#ifdef RSL_DEV_KNOBS
-// ---------------------------------------------------------------------------------------------
-// Fused front half at the cfg2 shape (S = 512, C = 128, packed work): K1 and K2 in ONE persistent launch whose packed
-// range spectra never leave the XCD's L2.  Each workgroup reads its XCD from HW_REG_XCC_ID and works only on that XCD's
-// share of the slabs (slab = one (frame, antenna)), from that XCD's queue of items in the order
-//   block b: K1 tiles (slab b, class c), c < 16;  then K2 tiles (slab b - kFrD, 16-bin tile t), t < 32,
-// so a K2 item always waits on K1 items dealt before it (to running workgroups): no deadlock.  Slab b's 16 K1 tiles
-// go into ring slot b % kFrR of that XCD's ring (kFrR slabs x 384 KiB = 2.3 MiB per XCD, inside its 4 MiB L2); its
-// K2 tiles wait until the slot's done counter shows the 16 K1 tiles, and a K1 tile for slab b waits until the K2
-// tiles of slab b - kFrR have read the slot.  Visibility is the XCD's own L2: the producer's stores complete
-// (s_waitcnt vmcnt(0), barrier) before one lane's counter add; the consumer polls by an atomic (memory side, never a
-// stale L2 copy) and reads the ring with nt loads (MI355X_MICROARCH: nt loads bypass the CU's L1 and are served by
-// the XCD's L2, where plain and nt stores keep their lines), so a line another CU rewrote is never read from a stale
-// L1.  Producer and consumer of a slot are always on one XCD (both chose the slab from their own XCD's queue).
-// Every wait is bounded (an error word is set and the item proceeds: wrong results, never a hang).
-// Development builds only (RSL_FRONT_FUSED=1; tools/front_fused_check.py): bit-identical to K1 + K2 but SLOWER, 6.62
-// against 5.08 ms per 2000 cfg2 frames (round 5).  LDS (43 KiB) holds it at 3 workgroups per CU, and the K2 tiles, which
-// reach 5.2 us per tile only by running 8 per CU, then expose their ring-load latency; claiming one item ahead with
-// the next K1 item's cube loads in flight made it worse (8.18 ms: the s_waitcnt before each done-count also waits for
-// those loads).  DESIGN.md section 4.
-constexpr int kFrR = 6, kFrD = 2;
-struct FrQueue {  // one 128-B line per counter
-  unsigned head[8][32];
-  unsigned done[8][kFrR][32];
-  unsigned cons[8][kFrR][32];
-  unsigned err[32];
-};
-constexpr size_t kFrRingBytes = (size_t)8 * kFrR * 16 * kPkTile;
-
-RSL_DEV unsigned fr_poll(unsigned* p) { return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// lane 0 of the workgroup waits until *p >= target (bounded), then the workgroup passes a barrier
-RSL_DEV void fr_wait(unsigned* p, unsigned target, unsigned* err) {
-  if (threadIdx.x == 0) {
-    unsigned it = 0;
-    // ~2^20 polls of >= 128 cycles (>= 50 ms) per wait; once any wait has timed out no workgroup waits again, so a
-    // broken hand-off ends the launch quickly (with wrong results and the error word set)
-    while (fr_poll(p) < target && fr_poll(err) == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 20)) {
-        atomicOr(err, 1u);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-template <int DBG = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_front_r512(const float2* __restrict__ cube, int Ct, int c0, int nslab,
-                                                          const float2* __restrict__ table,
-                                                          const float2* __restrict__ tw, int dc,
-                                                          unsigned char* __restrict__ ring, FrQueue* __restrict__ q,
-                                                          float2* __restrict__ rds, float thr_f, int i_lo, int i_hi,
-                                                          unsigned long long* __restrict__ mask,
-                                                          int* __restrict__ row_count, float* __restrict__ pk_pow) {
-  constexpr int S = 512, CB = 8, C = 128;
-  __shared__ float2 ldtab[S];
-  __shared__ float2 ldtw[32 * kR512TwPitch];
-  __shared__ float2 xbuf[CB * 16 * kR512Pitch];  // K1: stage exchange / output buffer; K2: its tile rows + exchange
-  static_assert(CB * kR512Obuf <= CB * 16 * kR512Pitch, "output buffer must fit in the exchange buffer");
-  static_assert(sizeof(float2) * 18 * kR128Pitch + 16 * 2 * 16 <= sizeof(float2) * CB * 16 * kR512Pitch,
-                "the K2 tile must fit in the exchange buffer");
-  __shared__ int s_item;
-  float2* obuf = xbuf;
-  const int tid = threadIdx.x;
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  const int x = (int)(xcc & 7u);
-  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
-  const int total = nx > 0 ? 48 * (nx + kFrD) : 0;
-  for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
-  for (int k = tid; k < 32 * 16; k += kThreads) {
-    const int jj = k >> 4, kk = k & 15;
-    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
-  }
-  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
-  for (;;) {
-    if (tid == 0) s_item = (int)atomicAdd(&q->head[x][0], 1u);
-    __syncthreads();
-    const int k = s_item;
-    __syncthreads();  // s_item is rewritten by the next claim
-    if (k >= total) break;
-    const int b = k / 48, r = k - 48 * (k / 48);
-    if (r < 16) {
-      // ---- K1 tile: chirp class r of slab b (k_range_fft_r512's body) ----
-      if (b >= nx) continue;
-      const int slot = b % kFrR;
-      fr_wait(&q->cons[x][slot][0], 32u * (unsigned)(b / kFrR), &q->err[0]);
-      // the thread index laundered per item: the compiler must not hoist this item's LDS table reads and addresses
-      // out of the item loop (they would stay live across the K2 items)
-      int lt = tid;
-      asm volatile("" : "+v"(lt));
-      const int row = lt >> 5, j = lt & 31;
-      const int k1b = (lt >> 1) & 15, h = lt & 1;
-      const int cb = r;
-      const long fa = (long)s0 + b;
-      float2 v[16];
-      {
-        const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 16 * row) * S + j;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = ld8<true>(src + 32 * m);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], ldtab[j + 32 * m]);
-      }
-      Dft<16>::run(v);
-#pragma unroll
-      for (int kk = 1; kk < 16; ++kk) v[kk] = cmul(v[kk], ldtw[j * kR512TwPitch + kk]);
-      float2* xw = xbuf + row * 16 * kR512Pitch + j;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) xw[kk * kR512Pitch] = v[kk];
-      __syncthreads();
-      const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
-      Dft<16>::run(v);
-      float2 xo[16];
-      const rsl_f2v sgn = h ? (rsl_f2v){-1.f, -1.f} : (rsl_f2v){1.f, 1.f};
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const float2 u = h ? cmul(v[kk], w32(kk)) : v[kk];
-        float2 recv;
-        recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0xB1, 0xF, 0xF, true));
-        recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0xB1, 0xF, 0xF, true));
-        xo[kk] = cf(__builtin_elementwise_fma(sgn, cv(u), cv(recv)));
-      }
-      if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);  // DC removal = zero range bin 0
-      __syncthreads();  // xbuf reads done: obuf aliases it
-      float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) ow[16 * kk] = xo[kk];
-      __syncthreads();
-      float2 y0[8], y1[8];
-      const int pos = 2 * lt + (lt >= 128 ? 8 : 0);
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) {
-        const float4 ab = *reinterpret_cast<const float4*>(obuf + qq * kR512Obuf + pos);
-        y0[qq] = make_float2(ab.x, ab.y);
-        y1[qq] = make_float2(ab.z, ab.w);
-      }
-      Dft<8>::run(y0);
-      Dft<8>::run(y1);
-#pragma unroll
-      for (int kk = 1; kk < 8; ++kk) {
-        const float2 wk = tw[4 * cb * kk];
-        y0[kk] = cmul(y0[kk], wk);
-        y1[kk] = cmul(y1[kk], wk);
-      }
-      float f0[16], f1[16];
-      unsigned m0 = 0u, m1 = 0u;
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) {
-        f0[2 * qq] = y0[qq].x;
-        f0[2 * qq + 1] = y0[qq].y;
-        f1[2 * qq] = y1[qq].x;
-        f1[2 * qq + 1] = y1[qq].y;
-        m0 = max(m0, max(__float_as_uint(y0[qq].x) & 0x7FFFFFFFu, __float_as_uint(y0[qq].y) & 0x7FFFFFFFu));
-        m1 = max(m1, max(__float_as_uint(y1[qq].x) & 0x7FFFFFFFu, __float_as_uint(y1[qq].y) & 0x7FFFFFFFu));
-      }
-      const int e0 = pk_exp(m0), e1 = pk_exp(m1);
-      uint4 w0[3], w1[3];
-      pk_pack16(f0, e0, w0);
-      pk_pack16(f1, e1, w1);
-      uint4* dst = reinterpret_cast<uint4*>(xring + ((size_t)slot * 16 + cb) * kPkTile) + lt;
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj) {
-        st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
-        st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's stores are in the L2 before the count
-      __syncthreads();  // obuf reads done (the next item rewrites it), every wave's stores waited for
-      if (tid == 0) __hip_atomic_fetch_add(&q->done[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      // ---- K2 tile: 16-bin tile r - 16 of slab b - kFrD (k_doppler_detect_r128's body) ----
-      const int bb = b - kFrD;
-      if (bb < 0 || bb >= nx) continue;
-      const int slot = bb % kFrR;
-      fr_wait(&q->done[x][slot][0], 16u * (unsigned)(bb / kFrR + 1), &q->err[0]);
-      constexpr int KB = 16, NR = KB + 2, NCB = 16, LD = kR128Pitch, SKL = kR128Skew, XPI = 8 * KB, XPH = 17;
-      float2* buf = xbuf;
-      float2* xi = buf;
-      float2* xh = buf + NCB * XPI;
-      const int k0 = (r - 16) * KB;
-      const unsigned fa = (unsigned)(s0 + bb);
-      const unsigned char* tiles = xring + (size_t)slot * 16 * kPkTile;
-      auto unit = [&](int kk, int cls, uint4(&w)[3]) {
-        const uint4* src = reinterpret_cast<const uint4*>(tiles + (size_t)cls * kPkTile +
-                                                          (size_t)(3 * (kk & 1)) * kPkPlane) + (kk >> 1);
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj)
-          w[jj] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + jj * (kPkPlane / 16))));
-      };
-      int lt = tid;
-      asm volatile("" : "+v"(lt));
-      const int bq = lt % KB, cls = lt / KB;
-      const bool halo = lt < 2 * NCB;
-      const int hside = lt >> 4, hcls = lt & 15;
-      // (wh and xv zero-initialised: an undefined value on the paths that skip them would be carried around the item
-      // loop in registers)
-      uint4 wi[3], wh[3] = {};
-      unit(k0 + bq, cls, wi);
-      if (halo) {
-        int kk = hside ? k0 + KB : k0 - 1;
-        kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
-        unit(kk, hcls, wh);
-      }
-      auto stage1 = [&](const uint4(&w)[3], float2* d, int st) {
-        float f[16];
-        pk_unpack16(w, f);
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) d[kk * st] = make_float2(f[2 * kk], f[2 * kk + 1]);
-      };
-      stage1(wi, xi + cls * XPI + bq, KB);
-      if (halo) stage1(wh, xh + hcls * XPH + hside, 2);
-      __syncthreads();  // every ring load of this tile has returned (its values are in LDS)
-      if (tid == 0) __hip_atomic_fetch_add(&q->cons[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool s2 = lt < 8 * NR;
-      const bool hs = lt >= 8 * KB;
-      const int k1 = hs ? (lt - 8 * KB) >> 1 : lt / KB;
-      const int b2 = hs ? ((lt & 1) ? NR - 1 : 0) : (lt % KB) + 1;
-      float2 xv[16] = {};
-      if (s2) {
-        const float2* src = hs ? xh + 2 * k1 + (lt & 1) : xi + lt;
-        const int cs = hs ? XPH : XPI;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) xv[c] = src[c * cs];
-        Dft<16>::run(xv);
-      }
-      __syncthreads();
-      if (s2) {
-        float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0);
-#pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) rw[k1 + 8 * k2] = xv[k2];
-      }
-      __syncthreads();
-      dd_tile_compute_reg<C, KB, 256, 0, LD, false, SKL>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds,
-                                                         thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow, lt);
-      __syncthreads();  // the tile's LDS reads done before the next item reuses xbuf
-    }
-  }
-}
-
-// The fused front half (k_front_r512) when the caller's work buffer holds the ring and the queue (F A >= 40 slabs at
-// cfg2) and no dB map is requested; returns hipErrorNotSupported otherwise (the two-kernel path runs).
-hipError_t launch_front_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
-                              const float2* table, const float2* tw_S, int dc, float2* work, size_t work_bytes,
-                              float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
-                              float* dbmap, float* pk_pow, int* pk_group) {
-  if (S != 512 || C != 128 || dbmap) return hipErrorNotSupported;
-  const size_t need = kFrRingBytes + sizeof(FrQueue);
-  if (work_bytes < need || (long)F * A < 8 * (kFrD + 1)) return hipErrorNotSupported;
-  unsigned char* ring = reinterpret_cast<unsigned char*>(work);
-  FrQueue* q = reinterpret_cast<FrQueue*>(ring + kFrRingBytes);
-  if (hipError_t e = hipMemsetAsync(q, 0, sizeof(FrQueue), st)) return e;
-  auto kern = k_front_r512<>;
-  const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, 1L << 30);
-  *pk_group = 16;  // tile-compact peak powers, as k_doppler_detect_r128
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), 0, st, cube, Ct, c0, F * A, table, tw_S, dc,
-                     reinterpret_cast<unsigned char*>(ring), q, rds, threshold_as_float(thr_p), i_lo, i_hi, mask,
-                     row_count, pk_pow);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// Front half as a PAIR of concurrent persistent kernels on two streams (development study, RSL_FRONT_PAIR=1): the L2
-// ring hand-off of k_front_r512, but each role with its own register / LDS budget and occupancy: k_front_k1p (the K1
-// body, 2 workgroups per CU) produces slab b's 16 class tiles into ring slot b % kFrR of its XCD, k_front_k2p (the K2
-// body, 3 workgroups per CU, 19 KiB each) consumes them.  Both claim their XCD's items in slab order from their own
-// queue heads; a K2 item waits for its slab's 16 done counts, a K1 item's stores wait until the slot's previous slab
-// has been read by its 32 K2 tiles.  Deadlock-free while each kernel has a resident workgroup on every XCD (the grids
-// leave room for each other on every CU: 2 x 43 + 3 x 19 KiB of LDS), and every wait is bounded as in k_front_r512.
-struct FpQueue {  // one 128-B line per counter
-  unsigned head1[8][32];
-  unsigned head2[8][32];
-  unsigned done[8][kFrR][32];
-  unsigned cons[8][kFrR][32];
-  unsigned err[32];
-};
-
-__global__ __launch_bounds__(kThreads) void k_front_k1p(const float2* __restrict__ cube, int Ct, int c0, int nslab,
-                                                         const float2* __restrict__ table,
-                                                         const float2* __restrict__ tw, int dc,
-                                                         unsigned char* __restrict__ ring, FpQueue* __restrict__ q) {
-  constexpr int S = 512, CB = 8;
-  __shared__ float2 ldtab[S];
-  __shared__ float2 ldtw[32 * kR512TwPitch];
-  __shared__ float2 xbuf[CB * 16 * kR512Pitch];
-  __shared__ int s_nn;
-  float2* obuf = xbuf;
-  const int tid = threadIdx.x;
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  const int x = (int)(xcc & 7u);
-  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
-  const int total = 16 * nx;
-  for (int k = tid; k < S; k += kThreads) ldtab[k] = table[k];
-  for (int k = tid; k < 32 * 16; k += kThreads) {
-    const int jj = k >> 4, kk = k & 15;
-    ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];
-  }
-  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
-  auto load = [&](float2(&nx_)[16], int t) {
-    int lt = tid;
-    asm volatile("" : "+v"(lt));
-    const int row = lt >> 5, j = lt & 31;
-    const float2* src = cube + ((size_t)(s0 + t / 16) * Ct + c0 + (t % 16) + 16 * row) * S + j;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) nx_[m] = ld8<true>(src + 32 * m);
-  };
-  if (tid == 0) s_nn = (int)atomicAdd(&q->head1[x][0], 1u);
-  __syncthreads();
-  int t = s_nn;
-  __syncthreads();
-  float2 nxv[16];
-  if (t < total) load(nxv, t);
-  while (t < total) {
-    unsigned claim = 0;
-    if (tid == 0) claim = atomicAdd(&q->head1[x][0], 1u);
-    int lt = tid;
-    asm volatile("" : "+v"(lt));
-    const int row = lt >> 5, j = lt & 31;
-    const int k1b = (lt >> 1) & 15, h = lt & 1;
-    const int b = t / 16, cb = t % 16, slot = b % kFrR;
-    float2 v[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = cmul(nxv[m], ldtab[j + 32 * m]);
-    // the next item is known once the claim issued above has returned: its cube loads start after stage 2
-    Dft<16>::run(v);
-#pragma unroll
-    for (int kk = 1; kk < 16; ++kk) v[kk] = cmul(v[kk], ldtw[j * kR512TwPitch + kk]);
-    float2* xw = xbuf + row * 16 * kR512Pitch + j;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) xw[kk * kR512Pitch] = v[kk];
-    __syncthreads();
-    const float2* xr = xbuf + (row * 16 + k1b) * kR512Pitch + h;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = xr[2 * i];
-    Dft<16>::run(v);
-    float2 xo[16];
-    const rsl_f2v sgn = h ? (rsl_f2v){-1.f, -1.f} : (rsl_f2v){1.f, 1.f};
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const float2 u = h ? cmul(v[kk], w32(kk)) : v[kk];
-      float2 recv;
-      recv.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.x), 0xB1, 0xF, 0xF, true));
-      recv.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(u.y), 0xB1, 0xF, 0xF, true));
-      xo[kk] = cf(__builtin_elementwise_fma(sgn, cv(u), cv(recv)));
-    }
-    if (dc && k1b == 0 && h == 0) xo[0] = make_float2(0.f, 0.f);
-    if (tid == 0) s_nn = (int)claim;
-    __syncthreads();
-    const int tn = s_nn;
-    float2* ow = obuf + row * kR512Obuf + k1b + 264 * h;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) ow[16 * kk] = xo[kk];
-    __syncthreads();
-    if (tn < total) load(nxv, tn);  // in flight during the Doppler step, the packing and the ring wait
-    float2 y0[8], y1[8];
-    const int pos = 2 * lt + (lt >= 128 ? 8 : 0);
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      const float4 ab = *reinterpret_cast<const float4*>(obuf + qq * kR512Obuf + pos);
-      y0[qq] = make_float2(ab.x, ab.y);
-      y1[qq] = make_float2(ab.z, ab.w);
-    }
-    Dft<8>::run(y0);
-    Dft<8>::run(y1);
-#pragma unroll
-    for (int kk = 1; kk < 8; ++kk) {
-      const float2 wk = tw[4 * cb * kk];
-      y0[kk] = cmul(y0[kk], wk);
-      y1[kk] = cmul(y1[kk], wk);
-    }
-    float f0[16], f1[16];
-    unsigned m0 = 0u, m1 = 0u;
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      f0[2 * qq] = y0[qq].x;
-      f0[2 * qq + 1] = y0[qq].y;
-      f1[2 * qq] = y1[qq].x;
-      f1[2 * qq + 1] = y1[qq].y;
-      m0 = max(m0, max(__float_as_uint(y0[qq].x) & 0x7FFFFFFFu, __float_as_uint(y0[qq].y) & 0x7FFFFFFFu));
-      m1 = max(m1, max(__float_as_uint(y1[qq].x) & 0x7FFFFFFFu, __float_as_uint(y1[qq].y) & 0x7FFFFFFFu));
-    }
-    const int e0 = pk_exp(m0), e1 = pk_exp(m1);
-    uint4 w0[3], w1[3];
-    pk_pack16(f0, e0, w0);
-    pk_pack16(f1, e1, w1);
-    fr_wait(&q->cons[x][slot][0], 32u * (unsigned)(b / kFrR), &q->err[0]);  // slab b - kFrR has left the slot
-    uint4* dst = reinterpret_cast<uint4*>(xring + ((size_t)slot * 16 + cb) * kPkTile) + lt;
-#pragma unroll
-    for (int jj = 0; jj < 3; ++jj) {
-      st16<true>(reinterpret_cast<float4*>(dst + jj * (kPkPlane / 16)), __builtin_bit_cast(float4, w0[jj]));
-      st16<true>(reinterpret_cast<float4*>(dst + (jj + 3) * (kPkPlane / 16)), __builtin_bit_cast(float4, w1[jj]));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&q->done[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = tn;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_front_k2p(int nslab, unsigned char* __restrict__ ring, FpQueue* __restrict__ q,
-                                                   float2* __restrict__ rds, float thr_f, int i_lo, int i_hi,
-                                                   unsigned long long* __restrict__ mask, int* __restrict__ row_count,
-                                                   float* __restrict__ pk_pow) {
-  constexpr int S = 512, C = 128, KB = 16, NR = KB + 2, NCB = 16, LD = kR128Pitch, SKL = kR128Skew, XPI = 8 * KB;
-  constexpr int XPH = 17;
-  extern __shared__ float2 sm[];
-  float2* buf = sm;
-  float2* xi = buf;
-  float2* xh = buf + NCB * XPI;
-  __shared__ int s_item;
-  const int tid = threadIdx.x;
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  const int x = (int)(xcc & 7u);
-  const int s0 = (int)((long)x * nslab / 8), nx = (int)((long)(x + 1) * nslab / 8) - s0;
-  const int total = 32 * nx;
-  unsigned char* xring = ring + (size_t)x * kFrR * 16 * kPkTile;
-  for (;;) {
-    if (tid == 0) s_item = (int)atomicAdd(&q->head2[x][0], 1u);
-    __syncthreads();
-    const int k = s_item;
-    __syncthreads();
-    if (k >= total) break;
-    const int bb = k / 32, slot = bb % kFrR;
-    fr_wait(&q->done[x][slot][0], 16u * (unsigned)(bb / kFrR + 1), &q->err[0]);
-    const int k0 = (k % 32) * KB;
-    const unsigned fa = (unsigned)(s0 + bb);
-    const unsigned char* tiles = xring + (size_t)slot * 16 * kPkTile;
-    auto unit = [&](int kk, int cls, uint4(&w)[3]) {
-      const uint4* src = reinterpret_cast<const uint4*>(tiles + (size_t)cls * kPkTile +
-                                                        (size_t)(3 * (kk & 1)) * kPkPlane) + (kk >> 1);
-#pragma unroll
-      for (int jj = 0; jj < 3; ++jj)
-        w[jj] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + jj * (kPkPlane / 16))));
-    };
-    int lt = tid;
-    asm volatile("" : "+v"(lt));
-    const int bq = lt % KB, cls = lt / KB;
-    const bool halo = (lt & 7) == 0;
-    const int hside = lt >> 7, hcls = (lt >> 3) & 15;
-    uint4 wi[3], wh[3] = {};
-    unit(k0 + bq, cls, wi);
-    if (halo) {
-      int kk = hside ? k0 + KB : k0 - 1;
-      kk = kk < 0 ? kk + S : (kk >= S ? kk - S : kk);
-      unit(kk, hcls, wh);
-    }
-    auto stage1 = [&](const uint4(&w)[3], float2* d, int st) {
-      float f[16];
-      pk_unpack16(w, f);
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) d[kk * st] = make_float2(f[2 * kk], f[2 * kk + 1]);
-    };
-    stage1(wi, xi + cls * XPI + bq, KB);
-    if (halo) stage1(wh, xh + hcls * XPH + hside, 2);
-    __syncthreads();  // every ring load of this tile has returned
-    if (tid == 0) __hip_atomic_fetch_add(&q->cons[x][slot][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool s2 = lt < 8 * NR;
-    const bool hs = lt >= 8 * KB;
-    const int k1 = hs ? (lt - 8 * KB) >> 1 : lt / KB;
-    const int b2 = hs ? ((lt & 1) ? NR - 1 : 0) : (lt % KB) + 1;
-    float2 xv[16] = {};
-    if (s2) {
-      const float2* src = hs ? xh + 2 * k1 + (lt & 1) : xi + lt;
-      const int cs = hs ? XPH : XPI;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) xv[c] = src[c * cs];
-      Dft<16>::run(xv);
-    }
-    __syncthreads();
-    if (s2) {
-      float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0);
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) rw[k1 + 8 * k2] = xv[k2];
-    }
-    __syncthreads();
-    dd_tile_compute_reg<C, KB, 256, 0, LD, false, SKL>(buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds,
-                                                       thr_f, i_lo, i_hi, mask, row_count, nullptr, pk_pow, lt);
-    __syncthreads();
-  }
-}
-
-hipError_t launch_front_pair(hipStream_t st, hipStream_t st2, hipEvent_t ev0, hipEvent_t ev1, const float2* cube,
-                             int F, int A, int Ct, int c0, int C, int S, const float2* table, const float2* tw_S, int dc,
-                             float2* work, size_t work_bytes, float2* rds, double thr_p, int i_lo, int i_hi,
-                             unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow, int* pk_group) {
-  if (S != 512 || C != 128 || dbmap || !st2 || !ev0 || !ev1) return hipErrorNotSupported;
-  const size_t need = kFrRingBytes + sizeof(FpQueue);
-  if (work_bytes < need || (long)F * A < 8) return hipErrorNotSupported;
-  unsigned char* ring = reinterpret_cast<unsigned char*>(work);
-  FpQueue* q = reinterpret_cast<FpQueue*>(ring + kFrRingBytes);
-  int dev = 0, ncu = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  int n1 = 2, n2 = 3;
-  if (const char* e = getenv("RSL_FRONT_PAIR_WG")) sscanf(e, "%d,%d", &n1, &n2);
-  const size_t lds2 = sizeof(float2) * 18 * kR128Pitch + 16 * 2 * 16;
-  if (hipError_t e = hipMemsetAsync(q, 0, sizeof(FpQueue), st)) return e;
-  if (hipError_t e = hipEventRecord(ev0, st)) return e;
-  if (hipError_t e = hipStreamWaitEvent(st2, ev0, 0)) return e;
-  *pk_group = 16;
-  const float thr_f = threshold_as_float(thr_p);
-  hipLaunchKernelGGL(k_front_k2p, dim3((unsigned)(n2 * ncu)), dim3(256), lds2, st2, F * A, ring, q, rds, thr_f, i_lo,
-                     i_hi, mask, row_count, pk_pow);
-  if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL(k_front_k1p, dim3((unsigned)(n1 * ncu)), dim3(kThreads), 0, st, cube, Ct, c0, F * A, table, tw_S,
-                     dc, ring, q);
-  if (hipError_t e = hipGetLastError()) return e;
-  if (hipError_t e = hipEventRecord(ev1, st2)) return e;
-  return hipStreamWaitEvent(st, ev1, 0);
-}
-#endif  // RSL_DEV_KNOBS
 
 template <int C>
 static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, int S, const float2* tw, float2* rds,
@@ -2305,10 +1772,6 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     if constexpr (S == 512 && CB == 8) {  // RSL_WORK_TEMPORAL=1: the packed `work` stored without the nt hint (MALL study)
       if (const char* e = getenv("RSL_WORK_TEMPORAL"))
         if (wexp && atoi(e) == 1) kern = k_range_fft_r512<true, 0, false>;
-    }
-    if constexpr (S == 512 && CB == 8) {  // RSL_R512_SWZ=1: XOR-swizzled LDS, 40 KiB, 4 workgroups per CU
-      if (const char* e = getenv("RSL_R512_SWZ"))
-        if (wexp && atoi(e) == 1) kern = k_range_fft_r512<true, 0, true, true>;
     }
     if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
       const int v = atoi(e);

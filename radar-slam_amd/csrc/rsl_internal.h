@@ -35,19 +35,6 @@ hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int 
 // bin's int8 exponent inside its 48-B unit; the pointer is only the switch, nothing is stored there) -- only where
 // work_packed_supported(C, S).
 bool work_packed_supported(int C, int S);
-#ifdef RSL_DEV_KNOBS
-// K1 + K2 fused at the cfg2 shape (rsl_fft.hip k_front_r512; a measured-slower development study):
-// hipErrorNotSupported when it does not apply.
-hipError_t launch_front_fused(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C, int S,
-                              const float2* table, const float2* tw_S, int dc, float2* work, size_t work_bytes,
-                              float2* rds, double thr_p, int i_lo, int i_hi, unsigned long long* mask, int* row_count,
-                              float* dbmap, float* pk_pow, int* pk_group);
-// K1 and K2 as two concurrent persistent kernels on st and st2 with the L2 ring hand-off (development study).
-hipError_t launch_front_pair(hipStream_t st, hipStream_t st2, hipEvent_t ev0, hipEvent_t ev1, const float2* cube,
-                             int F, int A, int Ct, int c0, int C, int S, const float2* table, const float2* tw_S, int dc,
-                             float2* work, size_t work_bytes, float2* rds, double thr_p, int i_lo, int i_hi,
-                             unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow, int* pk_group);
-#endif
 // K3: 3x3 local max (reflect), threshold, range gate -> per-antenna bit masks + row counts.
 hipError_t launch_detect(hipStream_t st, const float2* rds, int F, int A, int S, int C, double thr_p, int i_lo,
                          int i_hi, unsigned long long* mask, int* row_count, float* dbmap, float* pk_pow);

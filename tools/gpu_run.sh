@@ -55,14 +55,6 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab5_*.log ;;
     cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
-    fused) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fused 240 python -u tools/front_fused_check.py ;;
-    swz)  # K1 r512 with XOR-swizzled LDS (4 workgroups per CU, dev library RSL_R512_SWZ=1): outputs and bench A/B
-      CFG=cfg2 F=40 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_R512_SWZ=0 run swz_hash0 120 python -u tools/chain_hash.py
-      CFG=cfg2 F=40 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_R512_SWZ=1 run swz_hash1 120 python -u tools/chain_hash.py
-      tail -1 gpurun_out/${TAG}_swz_hash0.log; tail -1 gpurun_out/${TAG}_swz_hash1.log
-      for r in 1 2; do for v in 0 1; do RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_R512_SWZ=$v run swz${v}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
-      python3 tools/ab_summary.py gpurun_out/${TAG}_swz*_?.log ;;
-    pair) PAIR_WG_LIST='2,3;2,4;1,5;3,2' MODE=pair RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run pair 240 python -u tools/front_fused_check.py ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
         CFG=$c F=40 run hash_new_$c 120 python -u tools/chain_hash.py
