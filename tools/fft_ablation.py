@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import rsl  # noqa: E402
 from bench import make_cubes  # noqa: E402
 
-A, C, TC, F0 = {'cfg2': (8, 128, 51.2e-6, 2000), 'cfg5': (16, 256, 102.4e-6, 100)}[os.environ.get('CFG', 'cfg2')]
+A, C, TC, F0 = {'cfg2': (8, 128, 51.2e-6, 2000), 'cfg5': (16, 256, 102.4e-6, 100), 'cfg1': (8, 64, 25.6e-6, 4000)}[os.environ.get('CFG', 'cfg2')]
 F = int(os.environ.get('F', str(F0)))
 ctx = rsl.get_context(0)
 cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)

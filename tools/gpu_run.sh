@@ -54,6 +54,7 @@ for step in "$@"; do
         run ab5_new$r 200 python -u bench.py --config cfg5 --no-cpu-baseline
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab5_*.log ;;
+    cfg1abl) CFG=cfg1 ONLY0=1 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run cfg1abl 200 python -u tools/fft_ablation.py ;;
     cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
