@@ -99,7 +99,10 @@ int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double
  *     peak_pow is written group-compact: the peaks of the G rows r0 .. r0+G-1 of one (frame, antenna)
  *     (row = (f*A + a)*S + i, r0 a multiple of G) are contiguous from slot r0*C, in row order and Doppler order
  *     within a row (full cache lines instead of a short run per row).  *peak_pow_group (host, nullable)
- *     receives G (1 = row-compact, as rsl_detect writes it); pass it to rsl_peak_emit. */
+ *     receives G (1 = row-compact, as rsl_detect writes it); pass it to rsl_peak_emit.
+ *     work (c64-sized scratch, F A C S 8 bytes): at (S, C) = (256, 64), (512, 128) and (1024, 256) the range
+ *     spectra travel packed (6 B per value, chirp-class tiles) in its first F A C S 6 bytes and the rest is not
+ *     written; at other shapes it holds the c64 range spectra [F, A, C, S] as in rsl_rds. */
 int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
                    void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group);
