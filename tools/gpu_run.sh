@@ -55,6 +55,8 @@ for step in "$@"; do
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_ab5_*.log ;;
     cfg1abl) CFG=cfg1 ONLY0=1 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run cfg1abl 200 python -u tools/fft_ablation.py ;;
+    serialprof)  # kernel trace of the one-stream chain (standalone per-kernel times)
+      run serialprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_serial -o t -- python3 bench.py --pipeline 0 --no-cpu-baseline --no-pcie --no-extra ;;
     cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
