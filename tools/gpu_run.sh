@@ -19,6 +19,7 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     tests) run tests 560 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread ;;
+    tdoa) run tdoa 400 python -u -m pytest tests/test_gpu_doa_exact.py tests/test_gpu_chain.py tests/test_gpu_sweep.py tests/test_gpu_spectrum.py -x -q --timeout 150 --timeout-method thread ;;
     tsel) run tsel 400 python -u -m pytest tests/test_gpu_dbmap.py tests/test_gpu_doa_exact.py tests/test_gpu_chain.py tests/test_gpu_scheduling.py tests/test_gpu_pipelined.py -x -q --timeout 150 --timeout-method thread ;;
     testsall) run testsall 600 python -u -m pytest tests -m gpu -q --maxfail 12 --timeout 150 --timeout-method thread ;;
     doavar) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run doavar 300 python -u tools/doa_var_time.py 0
