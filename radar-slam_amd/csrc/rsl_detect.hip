@@ -304,7 +304,9 @@ RSL_DEV int block_exclusive_scan(int v, int* wsum, int& total) {
 
 // WPE: minimum waves per SIMD the register allocation must allow (0: unconstrained; A/B knob RSL_EMIT_WPE).
 // (Non-temporal entry stores were measured slower: 0.53 vs 0.48 ms per 1000 cfg2 frames.)
-template <int W, int MAXA, int WPE = 0>
+// CELLS = false: an entries-only launch (the cells go to k_emit_cells): no antenna-mask buffer in LDS (14 instead of 22
+// KiB) and no cell path in the registers.
+template <int W, int MAXA, int WPE = 0, bool CELLS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void k_emit_block(const unsigned long long* __restrict__ mask,
                                                     const unsigned long long* __restrict__ umask,
                                                     const float* __restrict__ pk_pow, int pk_group, long long F,
@@ -318,15 +320,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
                                                     int* __restrict__ c_frame, int* __restrict__ c_rc,
                                                     unsigned* __restrict__ c_amask) {
   static_assert(64 % W == 0, "a mask row must lie within one wave");
-  __shared__ unsigned pk[kEmitCap];   // item code: (word << 6) | bit
-  __shared__ unsigned pam[kEmitCap];  // cells: antenna mask of the item
+  __shared__ unsigned pk[kEmitCap];                  // item code: (word << 6) | bit
+  __shared__ unsigned pam[CELLS ? kEmitCap : 1];  // cells: antenna mask of the item
   __shared__ int wsum[4];
   __shared__ int s_cw[256], s_fi[256];
   __shared__ long long s_pkb[256];  // entries: peak_pow index of the word's item 0 minus its block rank
   __shared__ unsigned long long s_u[256];
   __shared__ long long s_first;
   const int t = threadIdx.x, lane = t & 63;
-  const bool entries = blockIdx.x < nblk_e;
+  const bool entries = !CELLS || blockIdx.x < nblk_e;
   const long long nent = F * A * S * W, ncw = F * S * W;
   const long long gw0 = (entries ? (long long)blockIdx.x : (long long)blockIdx.x - nblk_e) * 256;  // row-aligned
   const long long nw = entries ? nent : ncw;
@@ -357,8 +359,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
     for (int ww = 0; ww < W; ++ww)
       if (ww < w) cwo += __popcll(urow[ww]);
   }
-  unsigned long long ma[MAXA];  // cells: the antennas' peak words of (f, i, w)
-  if (!entries) {
+  unsigned long long ma[CELLS ? MAXA : 1];  // cells: the antennas' peak words of (f, i, w)
+  if (CELLS && !entries) {
 #pragma unroll
     for (int aa = 0; aa < MAXA; ++aa) ma[aa] = aa < A ? mask[(((size_t)f * A + aa) * S + i) * W + w] : 0ull;
   }
@@ -386,11 +388,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
         mm &= mm - 1;
         if (o >= base) {
           pk[o - base] = ((unsigned)t << 6) | (unsigned)b;
-          if (!entries) {
-            unsigned am = 0;
+          if constexpr (CELLS) {
+            if (!entries) {
+              unsigned am = 0;
 #pragma unroll
-            for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
-            pam[o - base] = am;
+              for (int aa = 0; aa < MAXA; ++aa) am |= (unsigned)((ma[aa] >> b) & 1ull) << aa;
+              pam[o - base] = am;
+            }
           }
         }
         ++o;
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
             if (e_pdb) e_pdb[e] = 10.0f * log10f(pw[uu] + 1e-12f);  // dechirp.py:235-236
           }
         }
-      } else {
+      } else if constexpr (CELLS) {
 #pragma unroll
         for (int uu = 0; uu < kEmitU; ++uu) {
           const int k = k0 + 256 * uu;
@@ -560,9 +564,12 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
     if (e != hipSuccess) return e;
   }
   // registers capped for 7 waves per SIMD (72 VGPRs, no spill; 7 workgroups per CU as the LDS allows, instead of 6):
-  // emit 0.45-0.47 vs 0.46-0.48 ms per 1000 cfg2 frames (tools/cpb.sh)
+  // emit 0.45-0.47 vs 0.46-0.48 ms per 1000 cfg2 frames (tools/cpb.sh); the entries-only instance (cells by
+  // k_emit_cells) holds 14 KiB of LDS and is capped for 8 waves per SIMD
+  constexpr int EWPE = 8;
 #define GO(WW)                                                                                                   \
-  hipLaunchKernelGGL((A <= 8 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 32>),                                   \
+  hipLaunchKernelGGL((cells4 ? (A <= 8 ? k_emit_block<WW, 8, EWPE, false> : k_emit_block<WW, 32, 0, false>)       \
+                             : (A <= 8 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 32>)),                         \
                      dim3(nb), dim3(256), 0, st, mask,                                                           \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
                      entry_cap, cell_cap, nbe, e_coord, e_cell, e_pdb, c_frame, c_rc, c_amask);
