@@ -281,7 +281,7 @@ constexpr double kTieRel = 1e-13;
 // over all 64 lanes.  Per grid tile (32 grid points) the two column tiles are two independent accumulator chains.
 template <int MA, int KB, bool MUSIC, bool GMAX, bool EXTRAS, int DBG = 0, int NTC = 0, bool SKEW = false,
           bool SPEC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (DBG == 11 ? 3 : 4) : (SPEC ? 1 : 3)))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4 : (SPEC ? 1 : 3)))) void k_doa_toep(const float2* __restrict__ rds, int A, int S, int C,
                                                   const int* __restrict__ cfr, const int* __restrict__ crc,
                                                   const long long* __restrict__ ncell_dev, long long ncell_host,
                                                   const uint4* __restrict__ ttab, int ntiles, int G,
@@ -309,24 +309,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   // Two-level prefetch: the signature of the next pass is loaded during this pass from cell indices that were loaded
   // one pass earlier (index loads followed at once by the dependent signature loads stalled every pass for a full
   // memory round trip).
-  constexpr bool PD2 = DBG == 11;  // ablation: signatures prefetched two passes ahead
-  float2 ns[MA], ns2[PD2 ? MA : 1];
+  // The next pass's signatures land in s itself, issued once this pass's prologue (the autocorrelation and the fused
+  // extras) has consumed s: no second signature array, and no register copies between passes (a separate prefetch
+  // array cost 16 64-bit moves per pass); the tile loop and the epilogue still cover the loads' latency.
+  float2 s[MA];
   int2 nidx = make_int2(0, 0);
   if (ch < nch) {
     const int c = ch * 64 + lane;
     if constexpr (DBG == 3) {
 #pragma unroll
-      for (int m = 0; m < MA; ++m) ns[m] = make_float2(0.1f * (lane + m), 0.2f * m - lane * 0.01f);
+      for (int m = 0; m < MA; ++m) s[m] = make_float2(0.1f * (lane + m), 0.2f * m - lane * 0.01f);
     } else {
-      load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, ns);
+      load_sig_c<MA>(rds, cfr, crc, c, c < ncell, A, plane, fstride, s);
       const int c2 = (ch + stride) * 64 + lane;
-      if constexpr (PD2) {
-        if (ch + stride < nch) load_sig_c<MA>(rds, cfr, crc, c2, c2 < ncell, A, plane, fstride, ns2);
-        const int c4 = (ch + 2 * stride) * 64 + lane;
-        if (ch + 2 * stride < nch) nidx = load_cell(cfr, crc, c4, c4 < ncell);
-      } else {
-        if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
-      }
+      if (ch + stride < nch) nidx = load_cell(cfr, crc, c2, c2 < ncell);
     }
   }
   // The argmax (and gmax) of a pass is stored at the start of the NEXT pass, after the wait for that pass's prefetched
@@ -338,29 +334,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
   int pidx = 0;
   float pgv = 0.f;
   for (; ch < nch; ch += stride) {
-    float2 s[MA];
-#pragma unroll
-    for (int m = 0; m < MA; ++m) s[m] = ns[m];
     if (pc >= 0) {
       out_idx[pc] = pidx;
       if constexpr (GMAX) out_gmax[pc] = pgv;
     }
     const int c = ch * 64 + lane;  // this lane's own cell
     const int nx = ch + stride;
-    if constexpr (PD2) {
-#pragma unroll
-      for (int m = 0; m < MA; ++m) ns[m] = ns2[m];
-      if (nx + stride < nch) {
-        load_sig_at<MA>(rds, nidx, A, plane, fstride, ns2);
-        const int c5 = (nx + 2 * stride) * 64 + lane;
-        if (nx + 2 * stride < nch) nidx = load_cell(cfr, crc, c5, c5 < ncell);
-      }
-    } else if (nx < nch && DBG != 3) {  // prefetch: the next pass's signatures, the pass after's cell indices
-      if constexpr (DBG == 10) nidx = make_int2(0, nidx.y & 2047);  // ablation: L2-resident signatures
-      load_sig_at<MA>(rds, nidx, A, plane, fstride, ns);
-      const int c3 = (nx + stride) * 64 + lane;
-      if (nx + stride < nch) nidx = load_cell(cfr, crc, c3, c3 < ncell);
-    }
     float ar[MA], ai[MA];
     acf<MA>(s, ar, ai);
     const float inv = ar[0] > 0.f ? kToepScale * __builtin_amdgcn_rcpf(ar[0]) : 0.f;
@@ -395,19 +374,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? (
           out_phase[c] = (double)atan2_fast(s[1].y * s[0].x - s[1].x * s[0].y, s[1].x * s[0].x + s[1].y * s[0].y);
       }
     }
+    // Prefetch into s: the next pass's signatures, the pass after's cell indices.  Unconditional: after the last pass
+    // nidx still holds this pass's cells (valid addresses, just read: cache hits), and a load under the loop-exit test
+    // would make s a phi of the loaded and the old values, i.e. a second register set and 16 copies per pass.
+    // The register barrier ends s's last uses (the compiler sinks the autocorrelation's tail below the extras, which
+    // kept s live beside its own prefetch: 16 copies at the loop latch).
+#pragma unroll
+    for (int k = 0; k < MA; ++k) asm volatile("" : "+v"(ar[k]), "+v"(ai[k])::"memory");
+    if constexpr (DBG != 3) {
+      if constexpr (DBG == 10) nidx = make_int2(0, nidx.y & 2047);  // ablation: L2-resident signatures
+      load_sig_at<MA>(rds, nidx, A, plane, fstride, s);
+      const int c3 = (nx + stride) * 64 + lane;
+      if (nx + stride < nch) nidx = load_cell(cfr, crc, c3, c3 < ncell);
+    }
     // B operands of the two column tiles: own K half from the own cell, the other half from lane ^ 32
     uint4 b0h[KB], b0l[KB], b1h[KB], b1l[KB];
     {
       uint4 eh[2 * KB], el[2 * KB];
-      if constexpr (DBG == 4) {
-        float e[16 * KB];
-#pragma unroll
-        for (int x = 0; x < 16 * KB; ++x) e[x] = s[x % MA].x;
-#pragma unroll
-        for (int q = 0; q < 2 * KB; ++q) split8(e + 8 * q, eh[q], el[q]);
-      } else {
-        toep_split<MA, KB>(ar, ai, inv, eh, el);
-      }
+      toep_split<MA, KB>(ar, ai, inv, eh, el);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         // E0 / E1 = the own cell's K rows 16 kb .. +7 / +8 .. +15.  Column tile 0 (cells of lanes 0-31) needs
@@ -907,7 +891,6 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
         if (v == 8) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 8, 12, true>;  // no argmax epilogue
         if (v == 9) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 9, 12, true>;  // no tile loop
         if (v == 10) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 10, 12, true>;  // L2-resident signatures
-        if (v == 11) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 11, 12, true>;  // prefetch 2 passes ahead
         if (v == 13) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 13, 12, true>;  // no second tracking
         if (v == 14) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 14, 12, true>;  // no in-tile count
         if (v == 15) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 15, 12, true>;  // second by one min
@@ -932,6 +915,14 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
   constexpr long long ppw = 8;
   long long blocks = (ncell_host + 256LL * ppw - 1) / (256LL * ppw);
   if (blocks < 1) blocks = 1;
+#ifdef RSL_DEV_KNOBS
+  // RSL_DOA_GRID: at most this many workgroups (the pass loop is grid-strided): a persistent share of the CUs, so
+  // that the scan co-runs with the other batch's memory-bound kernels instead of taking whole CUs (study)
+  if (const char* e = getenv("RSL_DOA_GRID")) {
+    const long long g = atoll(e);
+    if (g > 0 && blocks > g) blocks = g;
+  }
+#endif
   // ESPRIT's asin argument is clamped to [-1, 1] for d >= lambda / 2, where the reference's argument never exceeds 1
   // (|angle| <= pi) and only the fp32 rounding of pi * scale can; for d < lambda / 2, |x| > 1 gives NaN as in the
   // reference

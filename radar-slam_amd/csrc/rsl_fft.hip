@@ -1023,18 +1023,28 @@ constexpr bool dd_reg_ok() {
 // SKL: the last LDS row (NR - 1 = KB + 1, the upper halo row) starts SKL float2 after its pitch position (a bank skew of
 // the caller's row writes; k_doppler_detect_r128).
 // HSH: columns d >= C / 2 sit HSH float2 later in their row (k_doppler_detect_r256's bank shift).
-template <int C, int KB, int NT, int DBG = 0, int LD = lp_row(C) | 1, bool PADC = true, int SKL = 0, int HSH = 0>
+template <int C, int KB, int NT, int DBG = 0, int LD = lp_row(C) | 1, bool PADC = true, int SKL = 0, int HSH = 0,
+          bool UNI = false>
 RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, unsigned fa, float2* __restrict__ rds,
                                  float thr_f, int i_lo, int i_hi, unsigned long long* __restrict__ mask,
                                  int* __restrict__ row_count, float* __restrict__ dbmap,
                                  float* __restrict__ pk_pow, int tid_in = -1) {
   constexpr int NCH = C / 64;
   // tid_in: a laundered thread index from a persistent caller (keeps per-thread addresses out of its tile loop)
-  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, lane = tid & 63;
+  // UNI: the wave and tile indices are declared wave-uniform (readfirstlane), so the row index i, the range gate and
+  // the 'reflect' edge tests below are scalar instead of per-lane compares and selects: 884 -> 796 static VALU in
+  // k_doppler_detect_r128, 2.616-2.621 vs 2.640-2.642 ms per 2000 cfg2 frames (one call, outputs identical); in
+  // k_doppler_detect_r256 the same change measured slower (1.164 vs 1.144 ms per 100 configs[4] frames), so it is off
+  const int wave = UNI ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int ch = wave % NCH, rh = wave / NCH;
   const int j = ch * 64 + lane;  // shifted Doppler column: out[j] = X[(j - C//2) mod C]
   int d = j - C / 2;
   if (d < 0) d += C;
+  if constexpr (UNI) {  // tile-uniform (the callers' tile math reaches here as vector values)
+    fa = __builtin_amdgcn_readfirstlane(fa);
+    k0 = __builtin_amdgcn_readfirstlane(k0);
+  }
   int i0 = k0 + S / 2;  // shifted range row of LDS row 1
   if (i0 >= S) i0 -= S;
   const int rb = rh * 8;  // LDS rows rb .. rb + 9; interior rows rb + 1 .. rb + 8
@@ -1279,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
   float2* xh = buf + NCB * XPI;   // first write)
   const int tid = threadIdx.x;
   constexpr unsigned nkb = (unsigned)(S / KB);
-  const unsigned tile = (unsigned)xcd_tile(blockIdx.x, gridDim.x);
+  const unsigned tile = (unsigned)__builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(work);
   auto unit = [&](size_t tile0, int k, int cls, uint4(&w)[3]) {
     const uint4* src =
@@ -1340,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
     for (int k2 = 0; k2 < 16; ++k2) row[k1 + 8 * k2] = x[k2];
   }
   __syncthreads();
-  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL>(
+  dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL, 0, true>(
       buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
 }
 

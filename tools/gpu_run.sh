@@ -24,6 +24,17 @@ for step in "$@"; do
     testsall) run testsall 600 python -u -m pytest tests -m gpu -q --maxfail 12 --timeout 150 --timeout-method thread ;;
     doavar) RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run doavar 300 python -u tools/doa_var_time.py 0
       RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run doavar_ab 200 python -u tools/doa_var_time.py 0 ;;
+    doaab)  # DoA scan + fixup alone, product vs radar-slam_amd/lib/librsl_ab.so (tools/build_ab.sh), 2 rounds
+      for r in 1 2; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_ab.so run doaab_old$r 200 python -u tools/doa_var_time.py 0
+        run doaab_new$r 200 python -u tools/doa_var_time.py 0
+      done ;;
+    dgrid)  # DoA scan as a persistent share (dev library, RSL_DOA_GRID workgroups): pipelined bench + standalone DoA
+      for g in 0 256 512 768; do
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_DOA_GRID=$g run dgrid_b$g 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+        RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_DOA_GRID=$g run dgrid_d$g 200 python -u tools/doa_var_time.py 0
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_dgrid_b*.log ;;
     place)  # compaction / offsets placement in the pipelined step (RSL_BENCH_EMIT_BACK 0 / 1 / 2), 2 rounds
       for r in 1 2; do for p in 0 1 2; do RSL_BENCH_EMIT_BACK=$p run place${p}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_place*.log ;;
