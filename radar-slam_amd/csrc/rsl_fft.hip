@@ -576,7 +576,11 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
 constexpr int kR1kThreads = 512;
 constexpr int kPkPlane1k = 8 * 1024;        // bytes per plane of one S = 1024 tile (512 pairs x 16 B)
 constexpr int kPkTile1k = 6 * kPkPlane1k;   // bytes per tile
-RSL_DEV int r1k_tw(int j, int k) { return j * 16 + (k ^ ((j >> 1) & 15)); }  // W1024^(j k) in ldtw
+// W1024^(j k) in ldtw.  Swizzle (j / 2) ^ (j / 32): the stage-1 reads (lane j, one k) hit 64 distinct banks per 32-lane
+// group, and the stage-2 reads of rows j = 16 h (h = lane % 4: swizzles 0, 8, 1, 9) do too; with (j / 2) alone rows
+// 0 / 32 and 16 / 48 shared banks (2-way on 15 reads per tile and wave: most of the 17.2 M conflict cycles per 100
+// configs[4] frames, gpurun_out/r5aa_ddctr5)
+RSL_DEV int r1k_tw(int j, int k) { return j * 16 + (k ^ (((j >> 1) ^ (j >> 5)) & 15)); }
 
 template <bool DYN, int DBG = 0>
 __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_range_fft_r1024(const float2* __restrict__ cube, int A, int Ct,
@@ -1368,7 +1372,11 @@ __global__ __launch_bounds__(256) void k_doppler_detect_r128(const float2* __res
 // W32^(c k2) sum_r x[c + 32 r] W8^(r k1): the 256-point DFT exactly.  16 bins x 256 chirps on 512 threads, 37 KiB of
 // LDS: 4 workgroups (32 waves) per CU.  DBG (development builds only): 6 no work loads, 7 loads only.
 constexpr int kR256Pitch = 258;  // tile row pitch (float2): 256 columns + the HSH shift + 1 (516 b2 = 4 b2 mod 32 dwords)
-constexpr int kR256Skew = 1;
+// upper halo row: 6 float2 later, i.e. at 8 mod 16 positions (2 + 6) from row 0, so that each 16-lane group of the
+// halo wave's row writes (k1 of one parity x both sides x both h) covers 16 distinct bank pairs (skew 1 with k1 = u / 4:
+// 2- to 3-way on all 16 writes, ~76 of the 7.8 M conflict cycles per tile of 100 configs[4] frames, gpurun_out/r5aa_ddctr5)
+constexpr int kR256Skew = 6;
+constexpr int kR256Gap = 8;  // float2 between the tile rows (+ the skew's overhang) and the detection exchange words
 template <int DBG = 0>
 __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __restrict__ work, int S_arg,
                                                              const float2* __restrict__ tw, float2* __restrict__ rds,
@@ -1441,7 +1449,7 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
   const bool hs = tid >= 8 * KB * 2;  // threads 256-287: the halo rows
   const int u = tid - 8 * KB * 2;
   const int hh = tid & 1;
-  const int k1 = hs ? (u >> 2) : (tid >> 5);
+  const int k1 = hs ? 2 * ((u >> 2) & 3) + ((u >> 4) & 1) : (tid >> 5);  // halo: one k1 parity per 16-lane group
   const int side = (u >> 1) & 1;
   const int bi = (tid >> 1) & 15;
   const int b2 = hs ? (side ? NR - 1 : 0) : bi + 1;
@@ -1467,7 +1475,7 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
   }
   __syncthreads();
   dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL, HSH>(
-      buf, reinterpret_cast<float*>(buf + NR * LD), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
+      buf, reinterpret_cast<float*>(buf + NR * LD + kR256Gap), S, k0, fa, rds, thr_f, i_lo, i_hi, mask, row_count, dbmap, pk_pow);
 }
 
 // K2 + K3 for C = 64, S = 256 with packed `work` (the cfg1 shape; K1 = k_range_fft_r256): the Doppler FFT as 8 x 8.
@@ -1597,7 +1605,7 @@ static hipError_t launch_k2d_r256(hipStream_t st, const float2* work, int F, int
   static_assert(dd_reg_ok<C, KB, NT>(), "register tile body shape");
   if (S != 1024) return hipErrorInvalidValue;  // the kernel's tile math is compiled for S = 1024
   const long ntile = (long)F * A * (S / KB);
-  const size_t lds = sizeof(float2) * (size_t)(KB + 2) * kR256Pitch + (size_t)KB * (C / 64) * 16;
+  const size_t lds = sizeof(float2) * ((size_t)(KB + 2) * kR256Pitch + kR256Gap) + (size_t)KB * (C / 64) * 16;
   auto kern = k_doppler_detect_r256<>;
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_DD_DBG")) {  // ablation variants (development builds only; results are wrong)
