@@ -70,6 +70,7 @@ for step in "$@"; do
     serialprof)  # kernel trace of the one-stream chain (standalone per-kernel times)
       run serialprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_serial -o t -- python3 bench.py --pipeline 0 --no-cpu-baseline --no-pcie --no-extra ;;
     cfg5prof) run cfg5prof 600 bash tools/profile_cfg5.sh "$TAG" ;;
+    specprof) run specprof 600 bash tools/profile_spectrum.sh "$TAG" ;;
     hash)  # chain output hashes, product vs radar-slam_amd/lib/librsl_ab.so, cfg1 / cfg2 / cfg5
       for c in cfg1 cfg2 cfg5; do
         CFG=$c F=40 run hash_new_$c 120 python -u tools/chain_hash.py
