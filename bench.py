@@ -649,6 +649,10 @@ def chain_rooflines(r, A, C, S, F, config):
     if ks:
         out["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
     out["roofline_doa"] = entry('doa_scan', per('doa_scan'))
+    out["roofline_doa"]["timed"] = (
+        "hipEvents over the timed region (pipelined: the scan co-runs with the next batch's K1 / K2, which stretches "
+        "its span while the step gets shorter; the unshared rate is kernel_rooflines_standalone.doa_scan)" if ks
+        else "hipEvents over the timed region")
     out["kernel_rooflines_standalone"] = {k: entry(k, per_std(k)) for k in big if k in src_std}
     out["kernel_ms_per_step"] = {k: v[0] / max(v[1], 1) * (NS if k not in fft_names else Fl * NS / Ff)
                                  for k, v in kt.items() if v[1]}

@@ -35,6 +35,12 @@ for step in "$@"; do
         RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so RSL_DOA_GRID=$g run dgrid_d$g 200 python -u tools/doa_var_time.py 0
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_dgrid_b*.log ;;
+    pipe)  # pipelined two-stream step vs one stream (--pipeline 0), 2 rounds
+      for r in 1 2; do
+        run pipe1_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra
+        run pipe0_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra --pipeline 0
+      done
+      python3 tools/ab_summary.py gpurun_out/${TAG}_pipe*.log ;;
     place)  # compaction / offsets placement in the pipelined step (RSL_BENCH_EMIT_BACK 0 / 1 / 2), 2 rounds
       for r in 1 2; do for p in 0 1 2; do RSL_BENCH_EMIT_BACK=$p run place${p}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_place*.log ;;
