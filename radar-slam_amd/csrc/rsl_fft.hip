@@ -28,23 +28,28 @@ namespace rsl {
 
 constexpr int kThreads = 256;
 
-// K1 work queues (RSL_RF_DYN): per launch slot, 8 per-XCD dequeue heads and 8 exit counters, each on its own 128-B
-// line. The last workgroup of an XCD to leave resets its pair, so a slot is clean for its next launch.  A slot belongs
-// to one stream (rf_slot): launches on one stream run in order, so no two K1 launches in flight ever share a slot, for
-// up to kRfSlots streams per process (round 4 handed slots round-robin over all launches, which let the 8-slot ring
-// wrap onto a launch still queued on another stream: ADVICE r4).
-constexpr int kRfSlots = 64;
-__device__ unsigned g_rf_q[kRfSlots][2][8][32];
+// K1 work queues (RSL_RF_DYN): per stream, 8 per-XCD dequeue heads and 8 exit counters, each on its own 128-B line
+// ([2][8][32] unsigned, 2 KiB of device memory allocated and zeroed on the stream's first K1 launch).  The last
+// workgroup of an XCD to leave resets its pair, so the queue is clean for the stream's next launch; launches on one
+// stream run in order, so no two K1 launches in flight ever share a queue, for any number of streams (round 4 handed 8
+// slots round-robin over all launches, which let the ring wrap onto a launch still queued on another stream: ADVICE r4;
+// early round 5 kept 64 static slots per process, one per stream, which would wrap past 64 streams).
+constexpr size_t kRfQueueBytes = 2 * 8 * 32 * sizeof(unsigned);
 
-static int rf_slot(hipStream_t st) {
+static unsigned* rf_queue(hipStream_t st) {
   static std::mutex mu;
-  static std::unordered_map<hipStream_t, int> slots;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = slots.find(st);
-  if (it != slots.end()) return it->second;
-  const int s = (int)(slots.size() % kRfSlots);
-  slots.emplace(st, s);
-  return s;
+  static std::unordered_map<hipStream_t, unsigned*> queues;  // a destroyed stream's handle may come back: its queue
+  std::lock_guard<std::mutex> lock(mu);                        // is clean between launches, so reuse is safe
+  auto it = queues.find(st);
+  if (it != queues.end()) return it->second;
+  unsigned* q = nullptr;
+  if (hipMalloc(&q, kRfQueueBytes) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(q, 0, kRfQueueBytes, st) != hipSuccess) {  // ordered before the stream's first K1
+    (void)hipFree(q);
+    return nullptr;
+  }
+  queues.emplace(st, q);
+  return q;
 }
 
 // Global accesses with an optional non-temporal hint (`nt`: streamed once, not kept in L2 / MALL).
@@ -266,7 +271,7 @@ template <int S, int CB, bool DYN, int DBG = 0>
 __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                            int C, long ntile, const float2* __restrict__ table,
                                                            const float2* __restrict__ tw, int dc,
-                                                           float2* __restrict__ work, int slot,
+                                                           float2* __restrict__ work, unsigned* __restrict__ rfq,
                                                            unsigned char* __restrict__ wexp) {
   (void)wexp;
   constexpr int LD = lp_row(S);
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
-  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   // one tile: stage nx (x conj(ref) w) in LDS, refill nx with tile tn, FFT, DC bin, store
   auto body = [&](float4(&nx)[PF], long t, long tn) {
     unsigned claim = 0;
@@ -361,9 +366,9 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_p(const float2* __restri
       tn = s_nn;  // written before body's last barrier, rewritten only after the next body's first one
     }
     // every dequeue of this workgroup has returned: the XCD's last leaver resets the slot for its next launch
-    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+    if (tid == 0 && atomicAdd(head + 8 * 32, 1u) == (unsigned)gx - 1u) {
       atomicExch(head, 0u);
-      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+      atomicExch(head + 8 * 32, 0u);
     }
     return;
   }
@@ -406,7 +411,7 @@ template <bool DYN, int DBG = 0, bool NTW = true>
 __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                               int C, long ntile, const float2* __restrict__ table,
                                                               const float2* __restrict__ tw, int dc,
-                                                              float2* __restrict__ work, int slot,
+                                                              float2* __restrict__ work, unsigned* __restrict__ rfq,
                                                               unsigned char* __restrict__ wexp) {
   constexpr int S = 512, CB = 8;
   (void)wexp;  // the exponents travel inside the packed units (pk_pack16)
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
-  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
     unsigned claim = 0;
@@ -546,9 +551,9 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
       t = tn;
       tn = s_nn;
     }
-    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+    if (tid == 0 && atomicAdd(head + 8 * 32, 1u) == (unsigned)gx - 1u) {
       atomicExch(head, 0u);
-      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+      atomicExch(head + 8 * 32, 0u);
     }
     return;
   }
@@ -587,7 +592,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
                                                                   int c0, int C, long ntile,
                                                                   const float2* __restrict__ table,
                                                                   const float2* __restrict__ tw, int dc,
-                                                                  float2* __restrict__ work, int slot,
+                                                                  float2* __restrict__ work, unsigned* __restrict__ rfq,
                                                                   unsigned char* __restrict__ wexp) {
   constexpr int S = 1024, NT = kR1kThreads, ncb = 32;  // C = 256 wherever this kernel runs (work_packed_supported)
   (void)wexp;
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = DYN ? xcd * ntile / 8 : 0, hi = DYN ? (xcd + 1) * ntile / 8 : ntile;
-  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
     unsigned claim = 0;
@@ -736,9 +741,9 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
       t = tn;
       tn = *s_nn;
     }
-    if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+    if (tid == 0 && atomicAdd(head + 8 * 32, 1u) == (unsigned)gx - 1u) {
       atomicExch(head, 0u);
-      atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+      atomicExch(head + 8 * 32, 0u);
     }
     return;
   }
@@ -768,7 +773,7 @@ template <int DBG = 0>
 __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* __restrict__ cube, int A, int Ct, int c0,
                                                                  int C, long ntile, const float2* __restrict__ table,
                                                                  const float2* __restrict__ tw, int dc,
-                                                                 float2* __restrict__ work, int slot,
+                                                                 float2* __restrict__ work, unsigned* __restrict__ rfq,
                                                                  unsigned char* __restrict__ wexp) {
   constexpr int S = 256, NT = kR256Threads, ncb = 8;  // C = 64 wherever this kernel runs (work_packed_supported)
   (void)wexp;
@@ -804,7 +809,7 @@ __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* _
   const int xcd = blockIdx.x & 7;
   const long gx = (G - xcd + 7) / 8;
   const long lo = xcd * ntile / 8, hi = (xcd + 1) * ntile / 8;
-  unsigned* head = &g_rf_q[slot][0][xcd][0];
+  unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
     unsigned claim = 0;
@@ -886,9 +891,9 @@ __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* _
     t = tn;
     tn = s_nn;
   }
-  if (tid == 0 && atomicAdd(&g_rf_q[slot][1][xcd][0], 1u) == (unsigned)gx - 1u) {
+  if (tid == 0 && atomicAdd(head + 8 * 32, 1u) == (unsigned)gx - 1u) {
     atomicExch(head, 0u);
-    atomicExch(&g_rf_q[slot][1][xcd][0], 0u);
+    atomicExch(head + 8 * 32, 0u);
   }
 }
 
@@ -1737,9 +1742,10 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
   // per-XCD dequeue always applies (no static-walk instance)
   const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR1kThreads);
   if (nblk < 8) return hipErrorInvalidValue;
-  const int slot = rf_slot(st);
+  unsigned* rfq = rf_queue(st);
+  if (!rfq) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR1kThreads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
-                     work, slot, wexp);
+                     work, rfq, wexp);
   return hipGetLastError();
 }
 
@@ -1756,9 +1762,10 @@ static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int 
   // the per-XCD dequeue needs a workgroup on every XCD: tiny batches (F A < 1) do not occur (ntile >= 8)
   const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR256Threads);
   if (nblk < 8) return hipErrorInvalidValue;
-  const int slot = rf_slot(st);
+  unsigned* rfq = rf_queue(st);
+  if (!rfq) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR256Threads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
-                     work, slot, wexp);
+                     work, rfq, wexp);
   return hipGetLastError();
 }
 
@@ -1812,9 +1819,10 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       if (cap >= 8 && cap < nblk) nblk = cap;
     }
 #endif
-    int slot = 0;
+    unsigned* rfq = nullptr;
     if (nblk >= 8) {  // the per-XCD dequeue needs a workgroup on every XCD
-      slot = rf_slot(st);
+      rfq = rf_queue(st);
+      if (!rfq) return hipErrorOutOfMemory;
     } else {
       kern = k_range_fft_p<S, CB, false>;
       if constexpr (S == 512 && CB == 8) {
@@ -1822,7 +1830,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
       }
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), lds_k, st, cube, A, Ct, c0, C, ntile, table, tw,
-                       dc, work, slot, wexp);
+                       dc, work, rfq, wexp);
     return hipGetLastError();
   }
   const long nblk = (long)F * A * ((C + CB - 1) / CB);

@@ -99,6 +99,31 @@ def test_concurrent_streams(ctx):
                 assert torch.equal(_bits(a), _bits(b)), f'stream {k}: {w} differs on launch {rep}'
 
 
+def test_many_streams(ctx):
+    """More streams than round 5's first design had queue slots (64): each stream gets its own K1 dequeue queue
+    (rsl_fft.hip rf_queue), so 72 streams with a launch each in flight at once give the serial results bit for bit."""
+    import rsl
+    F, A, C, Tc = 2, 8, 128, 51.2e-6
+    g = torch.Generator(device='cuda').manual_seed(5)
+    ch0 = rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, ctx)
+    S = ch0.rds.shape[2]
+    cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
+                         torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
+    ref = _run(ctx, ch0, cube)
+    chains = [rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, ctx)
+              for _ in range(72)]
+    streams = [torch.cuda.Stream() for _ in chains]
+    torch.cuda.synchronize()
+    for ch, st in zip(chains, streams):
+        with torch.cuda.stream(st):
+            ctx.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                           row_count=ch.row_count, peak_pow=ch.peak_pow, dc_removal=True)
+    torch.cuda.synchronize()
+    for k, ch in enumerate(chains):
+        for a, b, w in zip((ref[1], ref[2], ref[3]), (ch.rds, ch.mask, ch.row_count), ('rds', 'mask', 'row_count')):
+            assert torch.equal(_bits(a), _bits(b)), f'stream {k}: {w} differs'
+
+
 @pytest.mark.parametrize('name', ['cfg1', 'cfg2', 'cfg5'])
 def test_chirp_window_packed(ctx, name):
     """A chirp window (chirp0 > 0 inside a longer cube) on the packed paths: K1 reads its class rows at the window's
