@@ -834,19 +834,40 @@ __global__ __launch_bounds__(256) void k_doa_fixup(const float2* __restrict__ rd
       vv[j].w = c0 + 3 < ncell ? out_idx[c0 + 3] : 0;
     }
   }
+  // Phase 1: queue the marked cells of all NST steps (the index registers die before any re-scan: interleaving the
+  // re-scans with the steps kept them live through it, 122 VGPRs and 4 waves per SIMD); phase 2: re-scan the queue.
 #pragma unroll
   for (int j = 0; j < NST; ++j) {
-    const int st = j * 256;
     const int v[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (v[k] < 0) q[wave][atomicAdd(&qn[wave], 1)] = make_int2(st + 4 * lane + k, v[k]);
+      if (v[k] < 0) {
+        const int slot = atomicAdd(&qn[wave], 1);
+        if (slot < kFixQ) q[wave][slot] = make_int2(j * 256 + 4 * lane + k, v[k]);
+      }
+  }
+  lds_sync();
+  const int nq = qn[wave];
+  rescan(min(nq, kFixQ));
+  if (nq > kFixQ) {  // more marked cells than the queue holds (wave-uniform; rare): the rest in rounds
+    __threadfence();  // the re-scanned cells' indices are written: the reloads below see them fixed (>= 0)
+    if (lane == 0) qn[wave] = 0;
     lds_sync();
-    const int n = qn[wave];
-    if (n >= 8 || st + 256 >= kFixCells) {  // full rounds now; the remainder after the last step
-      rescan(n);
-      if (lane == 0) qn[wave] = 0;
+#pragma unroll 1
+    for (int st = 0; st < kFixCells; st += 256) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long long c = base + st + 4 * lane + k;
+        const int v = c < ncell ? __hip_atomic_load(out_idx + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        if (v < 0) q[wave][atomicAdd(&qn[wave], 1)] = make_int2(st + 4 * lane + k, v);
+      }
       lds_sync();
+      const int n = qn[wave];
+      if (n >= 8 || st + 256 >= kFixCells) {
+        rescan(n);
+        if (lane == 0) qn[wave] = 0;
+        lds_sync();
+      }
     }
   }
 }

@@ -91,3 +91,39 @@ def test_exact_argmax_every_path(ctx, A, method):
         g = t.cpu().numpy()[:n]
         bad = np.nonzero(g != want)[0]
         assert len(bad) == 0, (path, [(int(i), int(g[i]), int(want[i])) for i in bad[:8]])
+
+
+@pytest.mark.parametrize('A', [8, 16])
+def test_fixup_queue_overflow(ctx, A):
+    """More marked cells in one re-scan wave's 2048-cell chunk than its LDS queue holds (264; rsl_doa_toep.hip
+    k_doa_fixup): 700 perfect steering vectors and halfway-phase cells, every one of them marked, so the rest after
+    the first queue load goes through the fixup's overflow rounds; every path must still give the fp64 argmax."""
+    import rsl
+    rs = np.random.RandomState(7 + A)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=64, chirp_duration=25.6e-6, method='music')
+    ch = rsl.RadarChain(cfg, 1, ctx)
+    grid = O.azimuth_grid()
+    steer = O.steering_matrix(grid, A)
+    phi = np.pi * np.sin(np.radians(grid))
+    m = np.arange(A)
+    sig = [np.exp(1j * phi[g] * m) for g in rs.randint(0, 361, 500)]
+    sig += [np.exp(1j * 0.5 * (phi[g] + phi[g + 1]) * m) for g in rs.randint(0, 360, 200)]
+    sig = np.array(sig).astype(np.complex64)
+    n = len(sig)
+    S, C = ch.S, ch.C
+    cells = np.sort(rs.choice(S * C, n, replace=False)).astype(np.int32)
+    rds = np.zeros((1, A, S, C), np.complex64)
+    rds[0, :, cells // C, cells % C] = sig
+    d_rds = ctx.to_dev(rds)
+    c_frame = ctx.to_dev(np.zeros(n, np.int32))
+    c_rc = ctx.to_dev(cells)
+    want = _expected(sig, steer, 'music')
+    got = {}
+    if ch.steer['toeplitz']:
+        got['toeplitz'] = ctx.doa(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n)[0]
+    got['f32'] = ctx.doa(d_rds, c_frame, c_rc, ch.steer, ch.method, n=n, fast=False)[0]
+    torch.cuda.synchronize()
+    for path, t in got.items():
+        g = t.cpu().numpy()[:n]
+        bad = np.nonzero(g != want)[0]
+        assert len(bad) == 0, (path, [(int(i), int(g[i]), int(want[i])) for i in bad[:8]])
