@@ -465,7 +465,9 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
         NS = 1
         vel2 = torch.empty((2, F, 8), dtype=torch.float64, device=dev)
         chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
-        sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        # RSL_BENCH_PRIO: stream priorities (front:back, torch's convention: lower = higher priority; 0:0 = equal)
+        pf, pb = (int(x) for x in os.environ.get('RSL_BENCH_PRIO', '0:0').split(':'))
+        sA, sB = torch.cuda.Stream(dev, priority=pf), torch.cuda.Stream(dev, priority=pb)
         cum = os.environ.get('RSL_BENCH_CUMASK')  # "front:back" CU counts: the two halves on CU-masked streams
         if cum:
             nf, nbk = (int(x) for x in cum.split(':'))
@@ -648,7 +650,12 @@ def chain_rooflines(r, A, C, S, F, config):
                                 "batch's DoA scan)" if ks else "hipEvents over the timed region")
     if ks:
         out["fft_stage_standalone"] = stage(ks, f"mean of {STANDALONE_RUNS} standalone launches after the timed region")
+        # the same stage's unshared rate beside the live one (the live spans include the other batch's co-running
+        # kernels: the pipelined step is shorter, each span longer)
+        out["roofline"]["frac_standalone"] = out["fft_stage_standalone"]["frac"]
     out["roofline_doa"] = entry('doa_scan', per('doa_scan'))
+    if ks and 'doa_scan' in src_std:
+        out["roofline_doa"]["frac_standalone"] = entry('doa_scan', per_std('doa_scan'))["frac"]
     out["roofline_doa"]["timed"] = (
         "hipEvents over the timed region (pipelined: the scan co-runs with the next batch's K1 / K2, which stretches "
         "its span while the step gets shorter; the unshared rate is kernel_rooflines_standalone.doa_scan)" if ks

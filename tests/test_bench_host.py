@@ -43,3 +43,21 @@ def test_pmc_traffic_named_kernels(tmp_path, monkeypatch):
     assert bench.pmc_traffic('k_doppler_detect_r128', 2000) == pytest.approx(15.4e9)
     assert bench.pmc_traffic('k_range_fft_p', 2000) is None  # a kernel the profile does not name: no bytes
     assert bench.pmc_traffic('k_range_fft_r512', 2000, config='cfg5') is None
+
+
+def test_chain_rooflines_live_and_standalone():
+    """The FFT-stage and DoA roofline objects carry the live fraction (hipEvent spans of the timed, pipelined steps)
+    and the same stage's standalone fraction; the standalone ones follow from kernel_ms_standalone."""
+    import bench
+    A, C, S, F = 8, 128, 512, 2000
+    kt = {'range_fft': (2.6 * 10, 10), 'doppler_fft': (2.8 * 10, 10), 'doa_scan': (5.7 * 10, 10), 'emit': (3.0, 10)}
+    ks = {'range_fft': (2.45 * 6, 6), 'doppler_fft': (2.62 * 6, 6), 'doa_scan': (3.44 * 6, 6)}
+    r = {'kt': kt, 'ks': ks, 'NS': 1, 'G': 361, 'nc': 71.9e6}
+    out = bench.chain_rooflines(r, A, C, S, F, 'cfg2')
+    alg = 2 * A * C * S * 8 * F
+    assert abs(out['roofline']['frac'] - alg / (5.4e-3) / 1e9 / bench.HBM_PEAK_GBS) < 1e-9
+    assert abs(out['roofline']['frac_standalone'] - alg / (5.07e-3) / 1e9 / bench.HBM_PEAK_GBS) < 1e-9
+    assert out['roofline']['frac_standalone'] == out['fft_stage_standalone']['frac']
+    flops = 3 * 2 * (2 * A - 1) * 71.9e6 * 361
+    assert abs(out['roofline_doa']['frac'] - flops / 5.7e-3 / 1e12 / bench.F16_MFMA_PEAK_TFLOPS) < 1e-9
+    assert abs(out['roofline_doa']['frac_standalone'] - flops / 3.44e-3 / 1e12 / bench.F16_MFMA_PEAK_TFLOPS) < 1e-9

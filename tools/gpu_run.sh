@@ -41,6 +41,16 @@ for step in "$@"; do
         run pipe0_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra --pipeline 0
       done
       python3 tools/ab_summary.py gpurun_out/${TAG}_pipe*.log ;;
+    prio)  # stream priorities of the pipelined halves (RSL_BENCH_PRIO front:back), 2 rounds
+      run prio_range 60 python -c "import torch; print(torch.cuda.Stream.priority_range())"
+      for r in 1 2; do
+        for pr in 0:0 -1:0 0:-1; do RSL_BENCH_PRIO=$pr run prio${pr/:/_}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done
+      done
+      cat gpurun_out/${TAG}_prio_range.log
+      for f in gpurun_out/${TAG}_prio*_?.log; do python3 -c "
+import json,sys
+l=[x for x in open(sys.argv[1]) if x.startswith('{')][-1]; d=json.loads(l)
+print(sys.argv[1], round(d['value']), 'fft live', round(d['roofline']['frac'],3), 'doa live', round(d['roofline_doa']['frac'],3))" $f; done ;;
     place)  # compaction / offsets placement in the pipelined step (RSL_BENCH_EMIT_BACK 0 / 1 / 2), 2 rounds
       for r in 1 2; do for p in 0 1 2; do RSL_BENCH_EMIT_BACK=$p run place${p}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_place*.log ;;
