@@ -902,6 +902,9 @@ static hipError_t launch_toep_t(hipStream_t st, const float2* rds, int A, int S,
     // outputs bit-identical (the spectrum scan keeps the rolled tile loop: the unrolled one spills with the stores)
     if (ntiles == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, true>;
   }
+  if constexpr (MA == 16 && !SPEC) {  // 16 antennas (KB = 2): the tile loop unrolled, no skew (that needs KB = 1)
+    if (ntiles == 12) kern = k_doa_toep<MA, KB, MUSIC, GMAX, EXTRAS, 0, 12, false>;
+  }
 #ifdef RSL_DEV_KNOBS
   if constexpr (MUSIC && !GMAX && !SPEC && MA == 8) {  // RSL_DOA_DBG: ablation variants of the skewed kernel (timing)
     if (const char* e = getenv("RSL_DOA_DBG")) {
