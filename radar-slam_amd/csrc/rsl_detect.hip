@@ -547,7 +547,8 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   if (cells4) {
     const unsigned nbc4 = (unsigned)(((long long)F * S * W) / kCellWords);
 #define GOC(WW)                                                                                                  \
-  hipLaunchKernelGGL((A <= 8 ? k_emit_cells<WW, 8> : k_emit_cells<WW, 32>), dim3(nbc4), dim3(256), 0, st, mask,  \
+  hipLaunchKernelGGL((A <= 8 ? k_emit_cells<WW, 8> : A <= 16 ? k_emit_cells<WW, 16> : k_emit_cells<WW, 32>),      \
+                     dim3(nbc4), dim3(256), 0, st, mask,                                                        \
                      umask, (long long)F, A, S, C, cell_row_off, cell_base, cell_cap, c_frame, c_rc, c_amask);
     switch (W) {
       case 1: GOC(1) break;
@@ -568,7 +569,7 @@ hipError_t launch_emit2(hipStream_t st, const unsigned long long* mask, const un
   // k_emit_cells) holds 14 KiB of LDS and is capped for 8 waves per SIMD
   constexpr int EWPE = 8;
 #define GO(WW)                                                                                                   \
-  hipLaunchKernelGGL((cells4 ? (A <= 8 ? k_emit_block<WW, 8, EWPE, false> : k_emit_block<WW, 32, 0, false>)       \
+  hipLaunchKernelGGL((cells4 ? k_emit_block<WW, 8, EWPE, false> /* entries only: MAXA unused */                 \
                              : (A <= 8 ? k_emit_block<WW, 8, 7> : k_emit_block<WW, 32>)),                         \
                      dim3(nb), dim3(256), 0, st, mask,                                                           \
                      umask, pk_pow, pk_group, (long long)F, A, S, C, entry_row_off, cell_row_off, entry_base, cell_base,     \
