@@ -668,7 +668,7 @@ def chain_rooflines(r, A, C, S, F, config):
     return out
 
 
-def configs_4_frame(ctx, dev, F=100, steps=4, warmup=2):
+def configs_4_frame(ctx, dev, F=400, steps=4, warmup=2):
     """Bounded sub-measurement of the configs[4] frame shape (A16 C256 S1024, the 1 M-frame 8-GPU workload's frame) on
     this GPU: the same full chain, pipelined, F frames per step, this rank only (no collective)."""
     import torch
@@ -694,7 +694,7 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--frames-per-step', type=int, default=None,
-                    help='frames per GPU per step (default 2000 for cfg2, 100 for cfg5)')
+                    help='frames per GPU per step (default 2000 for cfg2, 400 for cfg5)')
     ap.add_argument('--config', choices=('cfg2', 'cfg5', 'spectrum'), default='cfg2',
                     help='cfg2 = configs[2] (A8 C128 S512, the metric\'s workload); cfg5 = the configs[4] frame shape '
                          '(A16 C256 S1024); spectrum = configs[1] (A8 C128 S512, 1000 frames per step: RDS + peaks + '
@@ -745,7 +745,9 @@ def main():
     if args.config == 'spectrum':
         return run_spectrum(args, world, rank, local, dev)
     if args.config == 'cfg5':
-        A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 100
+        # 400 frames per step: the small per-batch kernels (offsets, one velocity workgroup per frame) fill the GPU
+        # (23.3 k vs 21.6 k frames/s at 100, gpurun_out/r5ad_cfg5f*); a 1 M-frame run batches at least this many
+        A, C, S, Tc, F = 16, 256, 1024, 102.4e-6, args.frames_per_step or 400
     else:
         A, C, S, Tc, F = 8, 128, 512, 51.2e-6, args.frames_per_step or 2000  # 5 steps = configs[2]'s 10 k frames
     ctx = rsl.get_context(local)

@@ -14,6 +14,6 @@ STATS=$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)
 mkdir -p profiles
 cp "$STATS" "profiles/${TAG}_cfg5_kernel_stats.csv"
 python3 tools/pmc_summary.py --stats "$STATS" --fetch "$OUT/fetch" --write "$OUT/write" \
-  --out "profiles/${TAG}_cfg5_pmc.json" --frames-per-launch 100 \
-  --note "bench.py --config cfg5 --steps 3 --warmup 1 (100 configs[4]-shape frames per launch); $(date -u)"
+  --out "profiles/${TAG}_cfg5_pmc.json" --frames-per-launch 400 \
+  --note "bench.py --config cfg5 --steps 3 --warmup 1 (400 configs[4]-shape frames per launch); $(date -u)"
 cp "profiles/${TAG}_cfg5_pmc.json" "profiles/${TAG}_cfg5_kernel_stats.csv" "$OUT/"
