@@ -1,5 +1,6 @@
 """Bit-identity of a K2 development variant against the default kernel on one cfg2 batch (development library):
-    RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so VAR=RSL_R128_X2 python tools/variant_check.py"""
+    RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so VAR=<knob> python tools/variant_check.py
+(VAR: a 0 / 1 development switch; round 3 used it for RSL_R128_X2, a variant since removed)"""
 import os
 import sys
 
@@ -11,7 +12,7 @@ import rsl  # noqa: E402
 from bench import make_cubes  # noqa: E402
 
 F = int(os.environ.get('F', '200'))
-var = os.environ.get('VAR', 'RSL_R128_X2')
+var = os.environ['VAR']
 ctx = rsl.get_context(0)
 cfg = rsl.ChainConfig(num_antennas=8, num_chirps=128, chirp_duration=51.2e-6)
 ch = rsl.RadarChain(cfg, F, ctx)
