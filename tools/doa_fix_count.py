@@ -1,5 +1,5 @@
 """How many cells k_doa_toep marks ambiguous (re-scanned in fp64 by k_doa_fixup) on the bench workload: one 2000-frame
-cfg2 chain with the fixup skipped (development library, RSL_DOA_NOFIX=1: marked cells keep -1 - index), and the DoA
+cfg2 chain (CFG=cfg5: 400 configs[4]-shape frames) with the fixup skipped (development library, RSL_DOA_NOFIX=1: marked cells keep -1 - index), and the DoA
 time (K5 + fixup, hipEvent scope) with and without the fixup.
 GPU box:  RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so python tools/doa_fix_count.py"""
 import os
@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import rsl  # noqa: E402
 from bench import make_cubes  # noqa: E402
 
-F, A, C, TC = 2000, 8, 128, 51.2e-6
+F, A, C, TC = {'cfg2': (2000, 8, 128, 51.2e-6), 'cfg5': (400, 16, 256, 102.4e-6)}[os.environ.get('CFG', 'cfg2')]
 ctx = rsl.get_context(0)
 cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=TC)
 ch = rsl.RadarChain(cfg, F, ctx)

@@ -57,6 +57,7 @@ print(sys.argv[1], round(d['value']), 'fft live', round(d['roofline']['frac'],3)
     cfg2f)  # cfg2 at 2000 / 4000 frames per step, 2 rounds
       for r in 1 2; do for f in 2000 4000; do run cfg2f${f}_$r 300 python -u bench.py --no-cpu-baseline --no-pcie --no-extra --frames-per-step $f; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_cfg2f*.log ;;
+    fixcount5) CFG=cfg5 RSL_LIBRARY=radar-slam_amd/lib/librsl_dev.so run fixcount5 300 python -u tools/doa_fix_count.py ;;
     place)  # compaction / offsets placement in the pipelined step (RSL_BENCH_EMIT_BACK 0 / 1 / 2), 2 rounds
       for r in 1 2; do for p in 0 1 2; do RSL_BENCH_EMIT_BACK=$p run place${p}_$r 200 python -u bench.py --no-cpu-baseline --no-pcie --no-extra; done; done
       python3 tools/ab_summary.py gpurun_out/${TAG}_place*.log ;;
