@@ -102,7 +102,9 @@ int rsl_detect(rsl_handle h, const void* rds, int F, int A, int S, int C, double
  *     receives G (1 = row-compact, as rsl_detect writes it); pass it to rsl_peak_emit.
  *     work (c64-sized scratch, F A C S 8 bytes): at (S, C) = (256, 64), (512, 128) and (1024, 256) the range
  *     spectra travel packed (6 B per value, chirp-class tiles) in its first F A C S 6 bytes and the rest is not
- *     written; at other shapes it holds the c64 range spectra [F, A, C, S] as in rsl_rds. */
+ *     written; at other shapes it holds the c64 range spectra [F, A, C, S] as in rsl_rds.
+ *     The range FFT's tile queue is per stream: the first call on a stream allocates 2 KiB of device memory
+ *     (kept for the process) and zeroes it on that stream (likewise rsl_rds). */
 int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp0, int C, int S,
                    const void* table, int dc_removal, void* work, void* rds, double thr_power, int i_lo, int i_hi,
                    void* mask, void* row_count, void* db_map, void* peak_pow, int* peak_pow_group);
