@@ -11,7 +11,12 @@
  *     complex values are interleaved float32 (c64) unless the name says c128 / f64;
  *   - all launches are asynchronous on the handle's stream (rsl_set_stream); rsl_sync waits;
  *   - return 0 (RSL_OK) or an RSL_ERR_* code; rsl_last_error(h) describes the last failure;
- *   - one handle per (device, stream); handles share no mutable state;
+ *   - a handle belongs to one device and may launch on any of that device's streams (rsl_set_stream); one thread
+ *     drives a handle at a time; handles share no mutable state (the K1 tile queues are per handle and stream,
+ *     allocated on the handle's device at a stream's first K1 launch, freed by rsl_destroy);
+ *   - graph capture: K1's first launch on a stream allocates that stream's queue, which capture forbids (RSL_ERR_HIP,
+ *     "operation not permitted when stream is capturing"): launch once uncaptured first, and never replay one captured
+ *     K1 on two streams concurrently (the replays would share the captured queue);
  *   - F = 0 (an empty batch) is valid: nothing is launched (rsl_peak_offsets zeroes the two bases), and
  *     buffers sized by F may be null;
  *   - capacity-sized lists (entries, cells) never overflow in memory: items past the capacity are dropped,
@@ -57,6 +62,12 @@ extern "C" {
 
 typedef struct rsl_context* rsl_handle;
 
+/* ABI version returned by rsl_version().
+ *   1  rounds 1-4;
+ *   2  rsl_rds_detect_chunked removed; rsl_steer_table_floats grew by the 4GM-float fp64 transposed section
+ *      (steer_t64_offset) that rsl_doa / rsl_doa_extras now read: tables built or sized by a v1 library must be
+ *      rebuilt; K1 tile queues are per handle and stream (freed by rsl_destroy). */
+#define RSL_VERSION 2
 int rsl_version(void);
 int rsl_create(rsl_handle* out, int device);
 int rsl_destroy(rsl_handle h);

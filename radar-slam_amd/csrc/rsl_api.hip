@@ -29,6 +29,7 @@ struct rsl_context {
   // the live timeline of the launches since the reset, every stream's launches on one device clock
   hipEvent_t t0 = nullptr;
   std::vector<std::pair<double, double>> span[RSL_K_COUNT];
+  rsl::RfQueues* rfq = nullptr;  // K1 tile queues, one per stream this handle launched K1 on (freed by rsl_destroy)
 };
 
 namespace {
@@ -84,19 +85,24 @@ float2* twiddles(rsl_context* h, int n) {
   return d;
 }
 
+// Folds the recorded launch events into the per-kernel totals and spans.  t0 is recorded on the stream bound at the
+// reset, which need not be the stream of a given launch: it is waited for once, and a span whose elapsed-time query
+// fails is dropped (never recorded as a silent (0, 0)); a failed duration query drops the launch from the totals.
 void collect(rsl_context* h) {
+  const bool t0_ok = h->t0 && hipEventSynchronize(h->t0) == hipSuccess;
   for (int k = 0; k < RSL_K_COUNT; ++k) {
     for (auto& p : h->ev[k]) {
       hipEventSynchronize(p.second);
       float ms = 0.f;
-      hipEventElapsedTime(&ms, p.first, p.second);
-      h->ms[k] += ms;
-      h->cnt[k] += 1;
-      if (h->t0) {
+      if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+        h->ms[k] += ms;
+        h->cnt[k] += 1;
+      }
+      if (t0_ok) {
         float a = 0.f, b = 0.f;
-        hipEventElapsedTime(&a, h->t0, p.first);
-        hipEventElapsedTime(&b, h->t0, p.second);
-        h->span[k].push_back({a, b});
+        if (hipEventElapsedTime(&a, h->t0, p.first) == hipSuccess &&
+            hipEventElapsedTime(&b, h->t0, p.second) == hipSuccess)
+          h->span[k].push_back({a, b});
       }
       h->ev_pool.push_back(p);
     }
@@ -108,7 +114,7 @@ void collect(rsl_context* h) {
 
 extern "C" {
 
-int rsl_version(void) { return 1; }
+int rsl_version(void) { return RSL_VERSION; }
 
 // 1: radix-{2,3,4,5,7,8} Stockham FFT in LDS; 2: any other length up to 4096 (direct DFT fallback); 0: no.
 int rsl_fft_supported(int n) {
@@ -127,6 +133,7 @@ int rsl_create(rsl_handle* out, int device) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RSL_ERR_HIP;
   rsl_context* h = new rsl_context();
   h->device = device;
+  h->rfq = rsl::rf_queues_new(device);
   *out = h;
   return RSL_OK;
 }
@@ -145,6 +152,7 @@ int rsl_destroy(rsl_handle h) {
     hipEventDestroy(p.second);
   }
   if (h->t0) hipEventDestroy(h->t0);
+  rsl::rf_queues_free(h->rfq);
   delete h;
   return RSL_OK;
 }
@@ -221,7 +229,7 @@ int rsl_rds(rsl_handle h, const void* cube, int F, int A, int C_total, int chirp
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                              dc_removal, (float2*)work, &sup);
+                              dc_removal, (float2*)work, &sup, h->rfq);
   }
   if (int r = hip_check(h, e, "range_fft")) return r;
   {
@@ -260,7 +268,7 @@ int rsl_rds_detect(rsl_handle h, const void* cube, int F, int A, int C_total, in
   {
     Scope sc(h, RSL_K_RANGE_FFT);
     e = rsl::launch_range_fft(h->stream, (const float2*)cube, F, A, C_total, chirp0, C, S, (const float2*)table, tS,
-                              dc_removal, (float2*)work, &sup, wexp);
+                              dc_removal, (float2*)work, &sup, h->rfq, wexp);
   }
   if (int r = hip_check(h, e, "range_fft")) return r;
   {

@@ -28,28 +28,66 @@ namespace rsl {
 
 constexpr int kThreads = 256;
 
-// K1 work queues (RSL_RF_DYN): per stream, 8 per-XCD dequeue heads and 8 exit counters, each on its own 128-B line
-// ([2][8][32] unsigned, 2 KiB of device memory allocated and zeroed on the stream's first K1 launch).  The last
-// workgroup of an XCD to leave resets its pair, so the queue is clean for the stream's next launch; launches on one
-// stream run in order, so no two K1 launches in flight ever share a queue, for any number of streams (round 4 handed 8
-// slots round-robin over all launches, which let the ring wrap onto a launch still queued on another stream: ADVICE r4;
-// early round 5 kept 64 static slots per process, one per stream, which would wrap past 64 streams).
+// K1 work queues (RSL_RF_DYN): per (handle, stream), 8 per-XCD dequeue heads and 8 exit counters, each on its own
+// 128-B line ([2][8][32] unsigned, 2 KiB of device memory allocated on the handle's device and zeroed on the stream's
+// first K1 launch through that handle).  The last workgroup of an XCD to leave resets its pair, so the queue is clean
+// for the stream's next launch; launches on one stream run in order, so no two K1 launches in flight ever share a
+// queue.  The set lives in the handle (rsl_context::rfq) and rsl_destroy frees it: handles share no mutable state
+// (rsl.h).  Round 5 kept one process-global map keyed by the stream handle alone, so two devices' null streams (both
+// handle 0, what torch reports for a default stream) shared one queue on the first device.
 constexpr size_t kRfQueueBytes = 2 * 8 * 32 * sizeof(unsigned);
 
-static unsigned* rf_queue(hipStream_t st) {
-  static std::mutex mu;
-  static std::unordered_map<hipStream_t, unsigned*> queues;  // a destroyed stream's handle may come back: its queue
-  std::lock_guard<std::mutex> lock(mu);                        // is clean between launches, so reuse is safe
-  auto it = queues.find(st);
-  if (it != queues.end()) return it->second;
-  unsigned* q = nullptr;
-  if (hipMalloc(&q, kRfQueueBytes) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(q, 0, kRfQueueBytes, st) != hipSuccess) {  // ordered before the stream's first K1
-    (void)hipFree(q);
-    return nullptr;
+struct RfQueues {
+  int device = 0;
+  std::mutex mu;
+  std::unordered_map<hipStream_t, unsigned*> q;  // a destroyed stream's address may come back on this handle's device:
+};                                               // its queue is clean between launches, so reuse is safe
+
+RfQueues* rf_queues_new(int device) {
+  RfQueues* s = new RfQueues();
+  s->device = device;
+  return s;
+}
+
+void rf_queues_free(RfQueues* s) {
+  if (!s) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(s->device);
+  for (auto& kv : s->q) (void)hipFree(kv.second);  // hipFree waits for the device: no K1 still reads the queue
+  (void)hipSetDevice(cur);
+  delete s;
+}
+
+// The queue of stream `st` in the set, allocated at its first use.  hipErrorStreamCaptureUnsupported when that first
+// use is inside a graph capture (hipMalloc is not capturable: run one uncaptured K1 launch on the stream first, and
+// never replay one captured K1 concurrently on two streams, which would share the captured queue); hipErrorInvalidDevice
+// when the stream belongs to another device than the handle.
+static hipError_t rf_queue(RfQueues* s, hipStream_t st, unsigned** out) {
+  *out = nullptr;
+  if (!s) return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> lock(s->mu);
+  auto it = s->q.find(st);
+  if (it != s->q.end()) {
+    *out = it->second;
+    return hipSuccess;
   }
-  queues.emplace(st, q);
-  return q;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+    return hipErrorStreamCaptureUnsupported;
+  hipDevice_t sd = 0;
+  if (st && hipStreamGetDevice(st, &sd) == hipSuccess && (int)sd != s->device) return hipErrorInvalidDevice;
+  unsigned* q = nullptr;
+  hipError_t e = hipMalloc(&q, kRfQueueBytes);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(q, 0, kRfQueueBytes, st);  // ordered before the stream's first K1
+  if (e != hipSuccess) {
+    (void)hipFree(q);
+    return e;
+  }
+  s->q.emplace(st, q);
+  *out = q;
+  return hipSuccess;
 }
 
 // Global accesses with an optional non-temporal hint (`nt`: streamed once, not kept in L2 / MALL).
@@ -1727,7 +1765,8 @@ static hipError_t launch_k2d(hipStream_t st, const float2* work, int F, int A, i
 
 // K1 at S = 1024 on packed work (work_packed_supported): k_range_fft_r1024, one tile per (frame, antenna, class).
 static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
-                                  const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+                                  const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp,
+                                  RfQueues* qs) {
   if (C != 256) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 256
   const long ntile = (long)F * A * 32;
   auto kern = k_range_fft_r1024<true>;
@@ -1742,8 +1781,8 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
   // per-XCD dequeue always applies (no static-walk instance)
   const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR1kThreads);
   if (nblk < 8) return hipErrorInvalidValue;
-  unsigned* rfq = rf_queue(st);
-  if (!rfq) return hipErrorOutOfMemory;
+  unsigned* rfq = nullptr;
+  if (hipError_t qe = rf_queue(qs, st, &rfq)) return qe;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR1kThreads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
                      work, rfq, wexp);
   return hipGetLastError();
@@ -1751,7 +1790,8 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
 
 // K1 at S = 256 on packed work (work_packed_supported): k_range_fft_r256, one tile per (frame, antenna, class).
 static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
-                                 const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+                                 const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp,
+                                 RfQueues* qs) {
   if (C != 64) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 64
   const long ntile = (long)F * A * 8;
   auto kern = k_range_fft_r256<>;
@@ -1762,8 +1802,8 @@ static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int 
   // the per-XCD dequeue needs a workgroup on every XCD: tiny batches (F A < 1) do not occur (ntile >= 8)
   const long nblk = resident_grid(reinterpret_cast<const void*>(kern), 0, ntile, kR256Threads);
   if (nblk < 8) return hipErrorInvalidValue;
-  unsigned* rfq = rf_queue(st);
-  if (!rfq) return hipErrorOutOfMemory;
+  unsigned* rfq = nullptr;
+  if (hipError_t qe = rf_queue(qs, st, &rfq)) return qe;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kR256Threads), 0, st, cube, A, Ct, c0, C, ntile, table, tw, dc,
                      work, rfq, wexp);
   return hipGetLastError();
@@ -1771,12 +1811,13 @@ static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int 
 
 template <int S>
 static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, int Ct, int c0, int C,
-                            const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp) {
+                            const float2* table, const float2* tw, int dc, float2* work, unsigned char* wexp,
+                            RfQueues* qs) {
   if constexpr (S == 1024) {
-    if (wexp) return launch_k1_r1024(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp);
+    if (wexp) return launch_k1_r1024(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp, qs);
   }
   if constexpr (S == 256) {
-    if (wexp) return launch_k1_r256(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp);
+    if (wexp) return launch_k1_r256(st, cube, F, A, Ct, c0, C, table, tw, dc, work, wexp, qs);
   }
   constexpr int CB = rows_for(S);
   if constexpr (S % 2 == 0 && (CB * (S / 2)) % kThreads == 0) {
@@ -1821,8 +1862,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
 #endif
     unsigned* rfq = nullptr;
     if (nblk >= 8) {  // the per-XCD dequeue needs a workgroup on every XCD
-      rfq = rf_queue(st);
-      if (!rfq) return hipErrorOutOfMemory;
+      if (hipError_t qe = rf_queue(qs, st, &rfq)) return qe;
     } else {
       kern = k_range_fft_p<S, CB, false>;
       if constexpr (S == 512 && CB == 8) {
@@ -1975,13 +2015,13 @@ hipError_t launch_doppler_detect(hipStream_t st, const float2* work, int F, int 
 
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
                             const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
-                            unsigned char* wexp) {
+                            RfQueues* queues, unsigned char* wexp) {
   *supported = true;
   if (F <= 0 || A <= 0 || C <= 0) return hipSuccess;
   switch (S) {
 #define CASE(n) \
   case n:       \
-    return launch_k1<n>(st, cube, F, A, Ct, chirp0, C, table, tw_S, dc, work, wexp);
+    return launch_k1<n>(st, cube, F, A, Ct, chirp0, C, table, tw_S, dc, work, wexp, queues);
     RSL_FFT_SIZES(CASE)
 #undef CASE
     default:

@@ -13,11 +13,16 @@ __device__ __forceinline__ long long list_count(const long long* dev, long long 
   return n < cap ? n : cap;
 }
 
+// K1 tile queues of one handle (rsl_fft.hip): one 2 KiB queue per stream the handle launches K1 on, allocated on the
+// handle's device at that stream's first K1 launch, freed by rf_queues_free (rsl_destroy).
+struct RfQueues;
+RfQueues* rf_queues_new(int device);
+void rf_queues_free(RfQueues* s);
 // K1: dechirp * window (table), range FFT (S points), DC bin zeroing.
 // cube c64 [F, A, Ct, S] (chirps chirp0 .. chirp0+C-1 used) -> work c64 [F, A, C, S]
 hipError_t launch_range_fft(hipStream_t st, const float2* cube, int F, int A, int Ct, int chirp0, int C, int S,
                             const float2* table, const float2* tw_S, int dc, float2* work, bool* supported,
-                            unsigned char* wexp = nullptr);
+                            RfQueues* queues, unsigned char* wexp = nullptr);
 // K2: Doppler FFT (C points) + fftshift on both axes, transposed store.
 // work c64 [F, A, C, S] -> rds c64 [F, A, S, C]
 hipError_t launch_doppler_fft(hipStream_t st, const float2* work, int F, int A, int C, int S, const float2* tw_C,

@@ -41,7 +41,7 @@ def test_c_host_compiles_links_and_runs(tmp_path):
                     '-L', LIB, '-lrsl', '-Wl,-rpath,' + LIB], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=120).stdout
     lines = dict(l.split(' ', 1) for l in out.strip().splitlines())
-    assert lines['version'] == '1'
+    assert lines['version'] == '2'
     assert lines['fft'] == '1 1 0'
     assert lines['steer'] == '1'
     assert lines['coord'] == '5 300 77'

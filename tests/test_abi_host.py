@@ -31,7 +31,7 @@ def test_library_exports_header():
     for n in names:
         assert hasattr(lib, n), f'{n} declared in rsl.h but not exported'
     assert sorted(_lib.SIGNATURES) == names, 'ctypes signature table out of sync with rsl.h'
-    assert lib.rsl_version() == 1
+    assert lib.rsl_version() == 2
 
 
 def test_library_reads_no_environment():

@@ -61,3 +61,32 @@ def test_chain_rooflines_live_and_standalone():
     flops = 3 * 2 * (2 * A - 1) * 71.9e6 * 361
     assert abs(out['roofline_doa']['frac'] - flops / 5.7e-3 / 1e12 / bench.F16_MFMA_PEAK_TFLOPS) < 1e-9
     assert abs(out['roofline_doa']['frac_standalone'] - flops / 3.44e-3 / 1e12 / bench.F16_MFMA_PEAK_TFLOPS) < 1e-9
+
+
+def _bench(args, env_extra, timeout=120):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_world_size_mismatch_exits():
+    """Under an external launcher whose WORLD_SIZE differs from --gpus the bench refuses to run (it would otherwise
+    time WORLD_SIZE ranks and report them as --gpus): non-zero exit before any device work."""
+    r = _bench(['--gpus', '8', '--steps', '1'], {'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0'})
+    assert r.returncode != 0 and 'WORLD_SIZE=1 but --gpus 8' in (r.stderr + r.stdout)
+    r = _bench(['--gpus', '0'], {})
+    assert r.returncode != 0
+
+
+def test_gpus_n_spawns_ranks_and_fails_loudly():
+    """`--gpus 2` with no launcher: the parent spawns two rank processes (RANK 0 / 1, WORLD_SIZE 2) and exits
+    non-zero when they fail.  Here (no device visible) every rank stops at its device check, so the exit code and the
+    rank's message show that the ranks were brought up and that a missing device is loud, never a 1-GPU run."""
+    r = _bench(['--gpus', '2', '--steps', '1', '--no-cpu-baseline'], {})
+    assert r.returncode != 0
+    err = r.stderr
+    assert 'needs device' in err and '--gpus 2' in err
+    assert 'terminating the other ranks' in err or err.count('needs device') == 2
+    assert not any(l.lstrip().startswith('{') for l in r.stdout.splitlines())

@@ -143,3 +143,39 @@ def test_chirp_window_packed(ctx, name):
     torch.cuda.synchronize()
     for a, b, w in zip(ref, bufs, ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
         assert torch.equal(_bits(a), _bits(b)), f'{name}: {w} differs for the chirp window'
+
+
+def test_two_handles_share_no_queue(ctx):
+    """K1's tile queues belong to the handle (rsl_context::rfq) and are keyed by stream inside it.
+    Two handles on device 0, both launching on the null stream (handle 0, what torch reports for a default stream,
+    the key every device's default stream shared in round 5's process-global map) and on one extra stream each, all
+    launches enqueued before any completes, give the serial results bit for bit; a handle destroyed and re-created
+    (its queues freed, new ones allocated at the same stream keys) still does."""
+    import rsl
+    F, A, C, Tc = 6, 8, 128, 51.2e-6
+    g = torch.Generator(device='cuda').manual_seed(17)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc)
+    ch0 = rsl.RadarChain(cfg, F, ctx)
+    S = ch0.rds.shape[2]
+    cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
+                         torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
+    ref = _run(ctx, ch0, cube)
+    for life in range(2):
+        hs = [rsl.Context(0), rsl.Context(0)]
+        null = torch.cuda.default_stream()  # cuda_stream == 0: the null stream
+        extra = [torch.cuda.Stream(), torch.cuda.Stream()]
+        jobs = [(h, st, rsl.RadarChain(cfg, F, h)) for h in hs for st in (null, extra[hs.index(h)])]
+        torch.cuda.synchronize()
+        for rep in range(4):
+            for h, st, ch in jobs:
+                with torch.cuda.stream(st):
+                    h.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                                 row_count=ch.row_count, peak_pow=ch.peak_pow, dc_removal=True)
+        torch.cuda.synchronize()
+        for k, (h, st, ch) in enumerate(jobs):
+            for a, b, w in zip((ref[1], ref[2], ref[3]), (ch.rds, ch.mask, ch.row_count), ('rds', 'mask', 'row_count')):
+                assert torch.equal(_bits(a), _bits(b)), f'life {life}, job {k}: {w} differs'
+        del jobs
+        for h in hs:
+            h.lib.rsl_destroy(h.h)
+            h.h = None
