@@ -65,12 +65,15 @@ GUARD_FILL = 0xA5
 
 class RadarChain:
     def __init__(self, cfg: ChainConfig, frames: int, ctx: Optional[Context] = None, vel_out=None,
-                 guard: bool = False):
+                 guard: bool = False, spec_out=None):
         """vel_out: optional device f64 [frames, 8] view receiving the per-frame velocity rows (lets several
         chains on different streams fill consecutive slices of one buffer).
         guard: debug canary — every device buffer of the chain gets its own allocation with GUARD_BYTES of sentinel
         bytes on both sides; guard_violations() lists the buffers whose pads were written (a store that left its own
-        buffer: tests/test_gpu_pipelined.py)."""
+        buffer: tests/test_gpu_pipelined.py).
+        spec_out: optional device f32 tensor receiving the cell-blocked spectrum (cfg.spectrum), of shape
+        spectrum_shape(), or 'contiguous': the chain allocates it with Context.empty_contiguous (one physically
+        contiguous allocation; the default allocator when the driver cannot provide one, spec_contiguous tells)."""
         self.cfg, self.F = cfg, int(frames)
         self.ctx = ctx or get_context()
         torch, ctx = self.ctx.torch, self.ctx
@@ -111,7 +114,25 @@ class RadarChain:
         self.ncell_dev = self.offs['cell_base'][F:F + 1]
         # one signature gather for DoA + ESPRIT + phase when the Toeplitz path applies (uniform linear array)
         self.fused_doa = bool(self.steer['toeplitz']) and A >= 2 and not cfg.spectrum
-        self.spec = e(((self.cell_cap + 31) // 32, len(self.grid), 32), torch.float32) if cfg.spectrum else None
+        self.spec = None
+        self.spec_contiguous = False
+        if cfg.spectrum:
+            shp = self.spectrum_shape()
+            if isinstance(spec_out, str):
+                if spec_out != 'contiguous':
+                    raise ValueError("spec_out: a tensor, 'contiguous' or None")
+                spec_out = ctx.empty_contiguous(shp, torch.float32)  # None: the driver could not provide it
+                self.spec_contiguous = spec_out is not None
+            if spec_out is not None:
+                if tuple(spec_out.shape) != shp or spec_out.dtype != torch.float32 or not spec_out.is_contiguous():
+                    raise ValueError(f'spec_out must be a contiguous float32 tensor of shape {shp}')
+                self.spec = spec_out
+            else:
+                self.spec = e(shp, torch.float32)
+
+    def spectrum_shape(self):
+        """Shape of the cell-blocked spectrum buffer: [ceil(cell_cap / 32), G, 32] f32."""
+        return ((self.cell_cap + 31) // 32, len(self.grid), 32)
 
     def _guarded_empty(self, shape, dtype):
         torch = self.ctx.torch

@@ -25,6 +25,39 @@ def unpack_coord(coord: np.ndarray):
     return ((u >> 26).astype(np.int32), ((u >> 13) & 0x1fff).astype(np.int32), (u & 0x1fff).astype(np.int32))
 
 
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime (libamdhip64, already loaded by torch-ROCm) for the few calls torch does not expose."""
+    global _HIP
+    if _HIP is None:
+        h = ctypes.CDLL('libamdhip64.so')
+        h.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        h.hipExtMallocWithFlags.restype = c_int
+        h.hipFree.argtypes = [c_void_p]
+        h.hipFree.restype = c_int
+        _HIP = h
+    return _HIP
+
+
+class _DeviceBlock:
+    """Owner of a raw device allocation exposed to torch through __cuda_array_interface__ (torch keeps this object
+    alive as long as the tensor's storage; hipFree when it goes)."""
+    _TYPESTR = {'float32': '<f4', 'float64': '<f8', 'int32': '<i4', 'int64': '<i8', 'complex64': '<c8', 'uint8': '|u1'}
+
+    def __init__(self, ptr, nbytes, shape, dtype, hip):
+        self.ptr, self.nbytes, self.hip = ptr, nbytes, hip
+        self.__cuda_array_interface__ = {'shape': tuple(int(d) for d in shape),
+                                         'typestr': self._TYPESTR[str(dtype).replace('torch.', '')],
+                                         'data': (ptr, False), 'version': 2, 'strides': None}
+
+    def __del__(self):
+        if self.ptr:
+            self.hip.hipFree(c_void_p(self.ptr))
+            self.ptr = 0
+
+
 def _ptr(t) -> Optional[c_void_p]:
     if t is None:
         return None
@@ -70,6 +103,25 @@ class Context:
 
     def empty(self, shape, dtype):
         return self.torch.empty(shape, dtype=dtype, device=self.device)
+
+    def empty_contiguous(self, shape, dtype):
+        """A device tensor in its own physically contiguous allocation (hipExtMallocWithFlags with
+        hipDeviceMallocContiguous), freed when the tensor goes away; None when the driver cannot provide it.  For the
+        large streamed outputs whose store rate depends on how the VRAM manager backs them (the configs[1] spectrum:
+        DESIGN §5)."""
+        torch = self.torch
+        n = 1
+        for d in shape:
+            n *= int(d)
+        nbytes = n * torch.empty((), dtype=dtype).element_size()
+        hip = _hip()
+        p = c_void_p()
+        torch.cuda.set_device(self.device)
+        if hip.hipExtMallocWithFlags(byref(p), ctypes.c_size_t(max(nbytes, 1)), 0x4) != 0 or not p.value:
+            hip.hipGetLastError()
+            return None
+        owner = _DeviceBlock(p.value, nbytes, shape, dtype, hip)
+        return torch.as_tensor(owner, device=self.device)
 
     def to_dev(self, arr: np.ndarray, dtype=None):
         t = self.torch.from_numpy(np.ascontiguousarray(arr))

@@ -137,3 +137,29 @@ def test_toeplitz_spectrum_matches_f32_scan(ctx, method):
           f'({(it != jf)[clear].sum()} with a clear gap)')
     assert err < DEN_ATOL
     assert (it == jf)[clear].all()
+
+
+def test_spectrum_contiguous_allocation(ctx):
+    """RadarChain(spec_out='contiguous') (the bench's configs[1] buffer): the spectrum lands in its own
+    physically contiguous allocation (Context.empty_contiguous) and is bit-identical to the default allocation's; a
+    spec_out tensor of the wrong shape is refused; the block is freed with the chain (allocated again at once)."""
+    import rsl
+    import torch
+    A, C, Tc = 8, 64, 25.6e-6
+    frames = _frames(A, C, Tc, 2)
+    cfg = rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc, spectrum=True, cell_frac=0.7)
+    cube = ctx.to_dev(frames.astype(np.complex64))
+    ref = rsl.RadarChain(cfg, 2, ctx)
+    ref.run(cube, esprit=False, velocity=False)
+    for _ in range(2):
+        ch = rsl.RadarChain(cfg, 2, ctx, spec_out='contiguous')
+        assert ch.spec_contiguous and tuple(ch.spec.shape) == ch.spectrum_shape()
+        ch.run(cube, esprit=False, velocity=False)
+        torch.cuda.synchronize()
+        nc = ch.totals()[1]
+        assert nc == ref.totals()[1]
+        from rsl.runtime import spectrum_rows
+        assert torch.equal(spectrum_rows(ch.spec, nc).view(torch.int32), spectrum_rows(ref.spec, nc).view(torch.int32))
+        del ch
+    with pytest.raises(ValueError):
+        rsl.RadarChain(cfg, 2, ctx, spec_out=torch.empty((3, 361, 32), device='cuda'))

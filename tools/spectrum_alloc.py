@@ -21,6 +21,8 @@ def main():
     ap.add_argument('--frames', type=int, default=1000)
     ap.add_argument('--reps', type=int, default=6)
     ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--contig', type=int, default=0, help='1: the spectrum in a physically contiguous allocation '
+                    '(RadarChain(spec_out=\'contiguous\'))')
     ap.add_argument('--pre-chain', type=int, default=0, help='first run the cfg2 chain bench.measure_chain (as the '
                     'default bench line does) before the spectrum allocations')
     args = ap.parse_args()
@@ -42,7 +44,10 @@ def main():
     for rep in range(args.reps):
         pad = pads[rep % len(pads)]
         hold = torch.empty(pad, dtype=torch.uint8, device=dev) if pad else None
-        ch = rsl.RadarChain(cfg, F, ctx)
+        t_alloc = time.perf_counter()
+        ch = rsl.RadarChain(cfg, F, ctx, spec_out='contiguous' if args.contig else None)
+        torch.cuda.synchronize()
+        t_alloc = time.perf_counter() - t_alloc
         ms = []
         for i in range(args.steps + 1):
             torch.cuda.synchronize()
@@ -58,7 +63,7 @@ def main():
                 ms.append({'wall': round(wall, 3), 'scan': round(kt['doa_scan'][0], 3),
                            'k1': round(kt['range_fft'][0], 3), 'k2': round(kt['doppler_fft'][0], 3)})
         p = ch.spec.data_ptr()
-        out = {'rep': rep, 'pad_MiB': pad >> 20, 'spec_ptr': hex(p), 'spec_GB': ch.spec.numel() * 4 / 1e9,
+        out = {'rep': rep, 'pad_MiB': pad >> 20, 'contiguous': ch.spec_contiguous, 'alloc_s': round(t_alloc, 3), 'spec_ptr': hex(p), 'spec_GB': ch.spec.numel() * 4 / 1e9,
                'ptr_mod_2M': p % (2 << 20), 'ptr_mod_1G': p % (1 << 30), 'rds_ptr': hex(ch.rds.data_ptr()),
                'steps': ms}
         print(json.dumps(out), flush=True)
