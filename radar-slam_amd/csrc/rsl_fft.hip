@@ -1496,25 +1496,38 @@ __global__ __launch_bounds__(512) void k_doppler_detect_r256(const float2* __res
   const int side = (u >> 1) & 1;
   const int bi = (tid >> 1) & 15;
   const int b2 = hs ? (side ? NR - 1 : 0) : bi + 1;
-  float2 x[16] = {};
+  float2 x[16];  // defined on the stage-2 lanes only: every use below is under s2
   if (s2) {
+    // hs is wave-uniform (waves 0-3: interior lanes only; wave 4: halo lanes 0-31, lanes 32-63 idle): a scalar branch,
+    // so that each path's 16 reads are one base address plus immediate offsets instead of both address forms and a
+    // select per read
+    if (__builtin_amdgcn_readfirstlane((int)hs)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = 2 * i + hh;
-      x[i] = hs ? xh[c * XPH + ((2 * k1 + side) ^ (c & 15))] : xi[c * XPI + ((16 * k1 + bi) ^ (16 * hh))];
+      for (int i = 0; i < 16; ++i) {
+        const int c = 2 * i + hh;
+        x[i] = xh[c * XPH + ((2 * k1 + side) ^ (c & 15))];
+      }
+    } else {
+      const float2* xb = xi + hh * XPI + ((16 * k1 + bi) ^ (16 * hh));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = xb[2 * i * XPI];
     }
     Dft<16>::run(x);
   }
   __syncthreads();  // exchange reads done: the tile rows alias it (each output is written as it forms)
-  const float sg = hh ? -1.f : 1.f;
-  float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0) + k1 + (C / 2 + HSH) * hh;
+  // the radix-2 step under s2 as a whole: waves 5-7 hold no stage-2 lane and skip it (they issued its ~175 VALU for
+  // nothing before); the lane pairs (h = 0, 1) of the DPP swap are both inside or both outside s2
+  if (s2) {
+    const float sg = hh ? -1.f : 1.f;
+    float2* rw = buf + b2 * LD + (b2 == NR - 1 ? SKL : 0) + k1 + (C / 2 + HSH) * hh;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float2 uu = hh ? cmul(x[k], w32(k)) : x[k];
-    float2 r;
-    r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.x), 0xB1, 0xF, 0xF, true));
-    r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.y), 0xB1, 0xF, 0xF, true));
-    if (s2) rw[8 * k] = make_float2(fmaf(sg, uu.x, r.x), fmaf(sg, uu.y, r.y));
+    for (int k = 0; k < 16; ++k) {
+      const float2 uu = hh ? cmul(x[k], w32(k)) : x[k];
+      float2 r;
+      r.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.x), 0xB1, 0xF, 0xF, true));
+      r.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(uu.y), 0xB1, 0xF, 0xF, true));
+      rw[8 * k] = make_float2(fmaf(sg, uu.x, r.x), fmaf(sg, uu.y, r.y));
+    }
   }
   __syncthreads();
   dd_tile_compute_reg<C, KB, NT, (DBG == 4 || DBG == 5 || DBG == 8 || DBG == 9) ? DBG : 0, LD, false, SKL, HSH>(
