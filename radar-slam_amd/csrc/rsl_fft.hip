@@ -1109,13 +1109,18 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
     return;
   }
   float vm[8];
+  if (i0 + rb > 0 && i0 + rb + 8 < S) {  // no row of this wave at a shifted range edge (30 of 32 tiles at cfg2)
 #pragma unroll
-  for (int rr = 0; rr < 8; ++rr) {
-    const int i = i0 + rb + rr;
-    float m = p[rr + 1];
-    if (i > 0) m = fmaxf(m, p[rr]);          // 'reflect' at the shifted range edges: no neighbour
-    if (i + 1 < S) m = fmaxf(m, p[rr + 2]);
-    vm[rr] = m;
+    for (int rr = 0; rr < 8; ++rr) vm[rr] = fmaxf(fmaxf(p[rr], p[rr + 1]), p[rr + 2]);  // v_max3_f32
+  } else {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int i = i0 + rb + rr;
+      float m = p[rr + 1];
+      if (i > 0) m = fmaxf(m, p[rr]);          // 'reflect' at the shifted range edges: no neighbour
+      if (i + 1 < S) m = fmaxf(m, p[rr + 2]);
+      vm[rr] = m;
+    }
   }
   // wave-edge columns for the horizontal neighbours: xch[(rh * 8 + rr) * 2 NCH + 2 ch + {0: lane 0, 1: lane 63}]
   float* ex = xch + (rb + 0) * 2 * NCH;
