@@ -179,3 +179,45 @@ def test_two_handles_share_no_queue(ctx):
         for h in hs:
             h.lib.rsl_destroy(h.h)
             h.h = None
+
+
+def test_k1_graph_capture(ctx):
+    """rsl.h's graph-capture rule: a handle's first K1 launch on a stream allocates that stream's tile queue, which a
+    capture forbids, so inside a capture it fails loudly (RuntimeError naming the capture) instead of invalidating the
+    capture; after one uncaptured launch on the stream, a captured K1 + K2 replays with the serial results bit for
+    bit."""
+    import rsl
+    F, A, C, Tc = 2, 8, 128, 51.2e-6
+    h = rsl.Context(0)  # a fresh handle: no queues yet
+    ch = rsl.RadarChain(rsl.ChainConfig(num_antennas=A, num_chirps=C, chirp_duration=Tc), F, h)
+    S = ch.rds.shape[2]
+    g = torch.Generator(device='cuda').manual_seed(23)
+    cube = torch.complex(torch.randn(F, A, C, S, device='cuda', generator=g),
+                         torch.randn(F, A, C, S, device='cuda', generator=g)) * 0.1
+    ref = _run(h, ch, cube)  # default stream: the handle's twiddle tables and that stream's queue
+
+    def launch():
+        h.rds_detect(cube, ch.table, ch.thr_p, ch.i_lo, ch.i_hi, rds=ch.rds, work=ch.work, mask=ch.mask,
+                     row_count=ch.row_count, peak_pow=ch.peak_pow, dc_removal=True)
+    st = torch.cuda.Stream()
+    with pytest.raises(RuntimeError, match='captur'):
+        with torch.cuda.graph(torch.cuda.CUDAGraph(), stream=st):
+            launch()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        launch()  # uncaptured: the queue of st
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=st):
+        launch()
+    for t in (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow):
+        t.zero_()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    for a, b, w in zip(ref, (ch.work, ch.rds, ch.mask, ch.row_count, ch.peak_pow),
+                       ('work', 'rds', 'mask', 'row_count', 'peak_pow')):
+        assert torch.equal(_bits(a), _bits(b)), f'{w} differs after graph replay'
+    h.lib.rsl_destroy(h.h)
+    h.h = None
