@@ -715,12 +715,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv):
+def launch_ranks(n, argv, script=None, grace=300.0):
     """`--gpus N` (N > 1) without an external launcher: bring up N rank processes of this script, one per GPU (rank r
     on device r), the way torch.distributed.run would, and relay rank 0's JSON line.  This process touches no GPU (it
     does not even import torch) and never execs: each rank is a fresh child (subprocess.Popen) with RANK, LOCAL_RANK,
     WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1 and MASTER_PORT in its environment.  If any rank exits
-    non-zero the others are terminated and this process exits with that rank's code (VERDICT r5 next #1)."""
+    non-zero the others are terminated and this process exits with that rank's code; ranks still
+    running ``grace`` seconds after another one finished are ended too (non-zero).  ``script``: the rank program
+    (default this file; tests substitute a stub)."""
     import subprocess
     import threading
     port = int(os.environ.get('MASTER_PORT') or _free_port())
@@ -728,8 +730,8 @@ def launch_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+        procs.append(subprocess.Popen([sys.executable, '-u', script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else 2, text=True))  # other ranks: fd 2
     lines = []
 
     def relay():  # rank 0's stdout (the JSON line and anything else it prints) to this process's stdout
@@ -741,17 +743,26 @@ def launch_ranks(n, argv):
     th.start()
     rc = 0
     live = set(range(n))
+    t_first = None  # when the first rank finished: the others get a grace period, then they are ended
     while live:
         for r in sorted(live):
             c = procs[r].poll()
             if c is None:
                 continue
             live.discard(r)
+            t_first = t_first or time.monotonic()
             if c != 0 and rc == 0:
                 rc = c if c > 0 else 1
                 sys.stderr.write(f'bench.py: rank {r} exited with {c}; terminating the other ranks\n')
                 for q in live:
                     procs[q].terminate()
+        if live and t_first is not None and time.monotonic() - t_first > grace:
+            sys.stderr.write(f'bench.py: ranks {sorted(live)} still running {grace:g} s after another rank finished; '
+                             'terminating them\n')
+            for q in live:
+                procs[q].terminate()
+            rc = rc or 1
+            t_first = time.monotonic() + 1e9  # terminate once; the loop then collects their exit codes
         time.sleep(0.05)
     th.join(timeout=10)
     if rc == 0 and not any(l.lstrip().startswith('{') for l in lines):

@@ -12,6 +12,11 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // scalar ops plus the register-pair shuffles its SLP vectoriser added around the scalar form.  Same roundings:
 // re = fma(a.x, b.x, -(a.y b.y)), im = fma(a.x, b.y, a.y b.x).
 typedef float rsl_f2v __attribute__((ext_vector_type(2)));
+// popcount of the bits of m below this lane, popc(m & ((1 << lane) - 1)), as v_mbcnt_lo + v_mbcnt_hi (2 VALU; the
+// compiler emits two ANDs and two v_bcnt for the popcount form)
+RSL_DEV int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
 RSL_DEV rsl_f2v cv(float2 a) { return __builtin_bit_cast(rsl_f2v, a); }
 RSL_DEV float2 cf(rsl_f2v v) { return __builtin_bit_cast(float2, v); }
 RSL_DEV float2 cadd(float2 a, float2 b) { return cf(cv(a) + cv(b)); }

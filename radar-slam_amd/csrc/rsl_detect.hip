@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_detect(const float2* __restrict__ rds, 
       const unsigned long long b = __ballot(pk);
       if (lane == 0) mask[((size_t)fa * S + i) * W + w] = b;
       if (pk_pow && pk)  // row-compact peak powers: slot = rank of the peak within its row
-        pk_pow[((size_t)fa * S + i) * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = mid[j];
+        pk_pow[((size_t)fa * S + i) * C + cnt + lanes_below(b)] = mid[j];
       cnt += __popcll(b);
     }
     if (lane == 0) row_count[(size_t)fa * S + i] = cnt;
@@ -233,7 +233,6 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
   const int lane = threadIdx.x & 63;
   const long f = row / S;
   const int i = (int)(row - f * S);
-  const unsigned long long lt = (1ull << lane) - 1ull;
   const unsigned long long* mf = mask + (size_t)f * A * S * W;
   const float2* rf = rds + (size_t)f * A * S * C;
   long long cnext = cell_base[f] + cell_row_off[row];
@@ -244,7 +243,7 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
     if (u == 0) continue;  // wave-uniform
     const int j = w * 64 + lane;
     const bool has = (u >> lane) & 1ull;
-    const long long c = cnext + __popcll(u & lt);
+    const long long c = cnext + lanes_below(u);
     unsigned am = 0;
     for (int a = 0; a < A; ++a) {
       const unsigned long long m = mf[((size_t)a * S + i) * W + w];
@@ -253,7 +252,7 @@ __global__ __launch_bounds__(256) void k_emit(const float2* __restrict__ rds, co
       if (hb) {
         am |= 1u << a;
         const unsigned long long* mrow = mf + ((size_t)a * S + i) * W;
-        long long e = e0 + entry_row_off[(size_t)f * A * S + (size_t)a * S + i] + __popcll(m & lt);
+        long long e = e0 + entry_row_off[(size_t)f * A * S + (size_t)a * S + i] + lanes_below(m);
         for (int ww = 0; ww < w; ++ww) e += __popcll(mrow[ww]);
         if (e < entry_cap) {
           e_coord[e] = ((unsigned)a << 26) | ((unsigned)i << 13) | (unsigned)j;

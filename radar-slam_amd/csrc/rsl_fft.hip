@@ -1041,7 +1041,7 @@ RSL_DEV void dd_tile_compute(float2* buf, const float2* tws, int S, int k0, unsi
       }
       const unsigned long long b = __ballot(pk);
       if (lane == 0) mask[row * W + w] = b;
-      if (pk_pow && pk) pk_pow[row * C + cnt + __popcll(b & ((1ull << lane) - 1ull))] = p;
+      if (pk_pow && pk) pk_pow[row * C + cnt + lanes_below(b)] = p;
       cnt += __popcll(b);
     }
     if (lane == 0) row_count[row] = cnt;
@@ -1159,7 +1159,6 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
   const int incl = wave_incl_scan(cw);
   const int excl = incl - cw;
   float* tile_pk = pk_pow ? pk_pow + ((size_t)fa * S + i0) * C : nullptr;
-  const unsigned long long lt = (1ull << lane) - 1ull;
   {
     // stage the tile's compacted peak powers in the (now dead) LDS tile, then one block-wide contiguous store of the
     // whole run instead of 8 partial-line stores per wave
@@ -1168,7 +1167,7 @@ RSL_DEV void dd_tile_compute_reg(const float2* buf, float* xch, int S, int k0, u
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       const int off = __builtin_amdgcn_readlane(excl, (rb + rr) * NCH + ch);
-      if (pkv[rr]) stg[off + __popcll(bal[rr] & lt)] = p[rr + 1];
+      if (pkv[rr]) stg[off + lanes_below(bal[rr])] = p[rr + 1];
     }
     __syncthreads();
     if (DBG != 4 && tile_pk)

@@ -90,3 +90,41 @@ def test_gpus_n_spawns_ranks_and_fails_loudly():
     assert 'needs device' in err and '--gpus 2' in err
     assert 'terminating the other ranks' in err or err.count('needs device') == 2
     assert not any(l.lstrip().startswith('{') for l in r.stdout.splitlines())
+
+
+STUB = r'''
+import json, os, sys, time
+r = int(os.environ['RANK'])
+mode = sys.argv[1]
+if mode == 'fail' and r == 1:
+    sys.exit(3)
+if mode == 'hang' and r == 1:
+    time.sleep(60)
+if r == 0:
+    print(json.dumps({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE',
+                                                  'MASTER_ADDR', 'MASTER_PORT')}), flush=True)
+'''
+
+
+@pytest.mark.parametrize('mode', ['ok', 'fail', 'hang'])
+def test_launch_ranks_protocol(tmp_path, mode, capsys):
+    """bench.launch_ranks with a stub rank program: every rank gets RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR = 127.0.0.1 / MASTER_PORT; rank 0's line is relayed; a failing rank's code is the
+    launcher's; a rank still running past the grace period after another finished is ended with a non-zero code."""
+    import bench
+    stub = tmp_path / 'stub.py'
+    stub.write_text(STUB)
+    t0 = __import__('time').monotonic()
+    rc = bench.launch_ranks(3, [mode], script=str(stub), grace=2.0)
+    took = __import__('time').monotonic() - t0
+    out = capsys.readouterr().out
+    lines = [json.loads(l) for l in out.splitlines() if l.startswith('{')]
+    if mode == 'ok':
+        assert rc == 0 and len(lines) == 1
+        e = lines[0]
+        assert e['RANK'] == '0' and e['LOCAL_RANK'] == '0' and e['WORLD_SIZE'] == '3' and e['LOCAL_WORLD_SIZE'] == '3'
+        assert e['MASTER_ADDR'] == '127.0.0.1' and int(e['MASTER_PORT']) > 0
+    elif mode == 'fail':
+        assert rc == 3
+    else:
+        assert rc != 0 and took < 30
