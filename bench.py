@@ -498,7 +498,10 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
         chains = [rsl.RadarChain(cfg, F // NS, ctx, vel_out=vel[k * (F // NS):(k + 1) * (F // NS)]) for k in range(NS)]
         streams = [torch.cuda.Stream(dev) for _ in range(NS)]
     # 0: offsets + compaction on the front stream; 1: compaction on the back stream; 2: both on the back stream
-    EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '1'))
+    # default 0 since round 6: 215.7-216.6 k vs 211.4-213.5 k frames/s with the compaction on the back stream (5 rounds
+    # alternating in one call, gpurun_out/r6ab_*): on the back stream it co-ran with the next K1 at 3 ms live
+    # instead of 0.7 and sat on the back half's critical path
+    EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '0'))
 
     def step_pipelined(i):
         k = i % 2
