@@ -477,8 +477,10 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     main = torch.cuda.current_stream(dev)
     if pipeline:
         NS = 1
-        vel2 = torch.empty((2, F, 8), dtype=torch.float64, device=dev)
-        chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(2)]
+        # RSL_BENCH_NBUF: chain buffers in flight (2: batch i + 1's front half waits for batch i - 1's back half)
+        NBUF = max(2, int(os.environ.get('RSL_BENCH_NBUF', '2')))
+        vel2 = torch.empty((NBUF, F, 8), dtype=torch.float64, device=dev)
+        chains = [rsl.RadarChain(cfg, F, ctx, vel_out=vel2[k]) for k in range(NBUF)]
         # RSL_BENCH_PRIO: stream priorities (front:back, torch's convention: lower = higher priority; 0:0 = equal)
         pf, pb = (int(x) for x in os.environ.get('RSL_BENCH_PRIO', '0:0').split(':'))
         sA, sB = torch.cuda.Stream(dev, priority=pf), torch.cuda.Stream(dev, priority=pb)
@@ -486,13 +488,13 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
         if cum:
             nf, nbk = (int(x) for x in cum.split(':'))
             sA, sB = cu_masked_stream(dev, nf, 0), cu_masked_stream(dev, nbk, 1)
-        evA = [torch.cuda.Event() for _ in range(2)]
-        evB = [torch.cuda.Event() for _ in range(2)]
+        evA = [torch.cuda.Event() for _ in range(NBUF)]
+        evB = [torch.cuda.Event() for _ in range(NBUF)]
         # the trajectory (scan, RCCL summary all-gather, pose gather to rank 0, smoothing) on a third stream, so the
         # collectives' latency stays off the back stream: batch i + 1's DoA does not wait for batch i's gather
         sC = torch.cuda.Stream(dev) if os.environ.get('RSL_BENCH_TRAJ_STREAM', '1') != '0' else None
-        evC = [torch.cuda.Event() for _ in range(2)]
-        used = [False, False]
+        evC = [torch.cuda.Event() for _ in range(NBUF)]
+        used = [False] * NBUF
     else:
         vel = torch.empty((F, 8), dtype=torch.float64, device=dev)
         chains = [rsl.RadarChain(cfg, F // NS, ctx, vel_out=vel[k * (F // NS):(k + 1) * (F // NS)]) for k in range(NS)]
@@ -504,7 +506,7 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     EMIT_BACK = int(os.environ.get('RSL_BENCH_EMIT_BACK', '0'))
 
     def step_pipelined(i):
-        k = i % 2
+        k = i % len(chains)
         ch = chains[k]
         sA.wait_stream(main)
         with torch.cuda.stream(sA):
@@ -542,7 +544,7 @@ def measure_chain(ctx, dev, A, C, Tc, F, steps, warmup, rank, world, *, ridge=0.
     for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
-    for ch in (chains[:min(warmup, 2)] if pipeline else chains):  # the chains that ran (pipelined: one per step)
+    for ch in (chains[:min(warmup, len(chains))] if pipeline else chains):  # the chains that ran (pipelined: one per step)
         ne, nc = ch.totals()
         if ne > ch.entry_cap or nc > ch.cell_cap:
             raise RuntimeError('peak capacity exceeded')
