@@ -548,9 +548,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     }
     Dft<8>::run(y0);
     Dft<8>::run(y1);
+    const int cbs = __builtin_amdgcn_readfirstlane(cb);  // the tile is workgroup-uniform
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
-      const float2 wk = tw[4 * cb * k];  // W128^(cb k) = W512^(4 cb k), 4 cb k <= 420 (workgroup-uniform)
+      const float2 wk = tw[4 * cbs * k];  // W128^(cb k) = W512^(4 cb k), 4 cb k <= 420 (workgroup-uniform: scalar loads)
       y0[k] = cmul(y0[k], wk);
       y1[k] = cmul(y1[k], wk);
     }
@@ -739,9 +740,10 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
     }
     Dft<8>::run(y0);
     Dft<8>::run(y1);
+    const int cbs = __builtin_amdgcn_readfirstlane(cb);  // the tile is workgroup-uniform
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
-      const float2 wk = tw[4 * cb * k];  // W256^(cb k) = W1024^(4 cb k), 4 cb k <= 868 (workgroup-uniform)
+      const float2 wk = tw[4 * cbs * k];  // W256^(cb k) = W1024^(4 cb k), 4 cb k <= 868 (workgroup-uniform: scalar loads)
       y0[k] = cmul(y0[k], wk);
       y1[k] = cmul(y1[k], wk);
     }
@@ -890,9 +892,10 @@ __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* _
     }
     Dft<8>::run(y0);
     Dft<8>::run(y1);
+    const int cbs = __builtin_amdgcn_readfirstlane(cb);  // the tile is workgroup-uniform
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
-      const float2 wk = tw[4 * cb * k];  // W64^(cb k) = W256^(4 cb k), 4 cb k <= 196 (workgroup-uniform)
+      const float2 wk = tw[4 * cbs * k];  // W64^(cb k) = W256^(4 cb k), 4 cb k <= 196 (workgroup-uniform: scalar loads)
       y0[k] = cmul(y0[k], wk);
       y1[k] = cmul(y1[k], wk);
     }
