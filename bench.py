@@ -30,11 +30,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
 DIST = False  # a torch.distributed process group is up (set in main)
-PROFILE = os.path.join(ROOT, 'profiles', 'r6n_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r6o_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
-CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r6n_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
+CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r6o_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
 STANDALONE_RUNS = 6  # unpipelined chain runs after the timed region (kernel_ms_standalone, fft_stage_standalone)
 TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
                   ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')
