@@ -470,6 +470,7 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
     ldtw[jj * kR512TwPitch + kk] = tw[jj * kk];  // W512^(j k1), j k1 <= 465
   }
   auto load = [&](float2(&nx)[16], long t) {
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);  // the tile index is workgroup-uniform (ntile < 2^31)
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
     const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 16 * row) * S + j;  // chirp class cb, row q = row
@@ -488,6 +489,10 @@ __global__ __launch_bounds__(kThreads) void k_range_fft_r512(const float2* __res
   unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
+    // workgroup-uniform tile indices (read from LDS or derived from blockIdx; ntile < 2^31, checked by the launcher):
+    // scalar, so the tile's address arithmetic runs on the SALU
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);
+    tn = (long)__builtin_amdgcn_readfirstlane((int)tn);
     unsigned claim = 0;
     if (DYN && tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
@@ -651,6 +656,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (kk) ldtw[r1k_tw(jj, kk)] = tw[jj * kk];  // W1024^(j k1), j k1 <= 945 (k1 = 0: never read)
   }
   auto load = [&](float2(&nx)[16], long t) {
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);  // the tile index is workgroup-uniform (ntile < 2^31)
     int lt = tid;
     asm volatile("" : "+v"(lt));
     const int row = lt >> 6, j = lt & 63;
@@ -671,6 +677,10 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
   unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
+    // workgroup-uniform tile indices (read from LDS or derived from blockIdx; ntile < 2^31, checked by the launcher):
+    // scalar, so the tile's address arithmetic runs on the SALU
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);
+    tn = (long)__builtin_amdgcn_readfirstlane((int)tn);
     unsigned claim = 0;
     if (DYN && tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
@@ -832,6 +842,7 @@ __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* _
     ldtw[r256_tw(jj, kk)] = tw[jj * kk];  // W256^(j k1), j k1 <= 225
   }
   auto load = [&](float2(&nx)[16], long t) {
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);  // the tile index is workgroup-uniform (ntile < 2^31)
     int lt = tid;
     asm volatile("" : "+v"(lt));
     const int row = lt >> 4, j = lt & 15;
@@ -852,6 +863,10 @@ __global__ __launch_bounds__(kR256Threads) void k_range_fft_r256(const float2* _
   unsigned* head = rfq + xcd * 32;  // this XCD's dequeue head (the exit counter: + 256)
   __syncthreads();
   auto body = [&](float2(&nx)[16], long t, long tn) {
+    // workgroup-uniform tile indices (read from LDS or derived from blockIdx; ntile < 2^31, checked by the launcher):
+    // scalar, so the tile's address arithmetic runs on the SALU
+    t = (long)__builtin_amdgcn_readfirstlane((int)t);
+    tn = (long)__builtin_amdgcn_readfirstlane((int)tn);
     unsigned claim = 0;
     if (tid == 0) claim = atomicAdd(head, 1u);
     const int cb = (int)(t % ncb);
@@ -1789,6 +1804,7 @@ static hipError_t launch_k1_r1024(hipStream_t st, const float2* cube, int F, int
                                   RfQueues* qs) {
   if (C != 256) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 256
   const long ntile = (long)F * A * 32;
+  if (ntile >= (1L << 31)) return hipErrorInvalidValue;  // the kernel's tile indices are 32-bit (readfirstlane)
   auto kern = k_range_fft_r1024<true>;
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_RF_DBG")) {  // ablation (development builds only; results are wrong)
@@ -1814,6 +1830,7 @@ static hipError_t launch_k1_r256(hipStream_t st, const float2* cube, int F, int 
                                  RfQueues* qs) {
   if (C != 64) return hipErrorInvalidValue;  // its chirp-class tiles are compiled for C = 64
   const long ntile = (long)F * A * 8;
+  if (ntile >= (1L << 31)) return hipErrorInvalidValue;  // the kernel's tile indices are 32-bit (readfirstlane)
   auto kern = k_range_fft_r256<>;
 #ifdef RSL_DEV_KNOBS
   if (const char* e = getenv("RSL_RF_DBG"))  // ablation (development builds only; results are wrong)
@@ -1844,6 +1861,7 @@ static hipError_t launch_k1(hipStream_t st, const float2* cube, int F, int A, in
     // 8 chirp rows per tile at S = 512: 16 rows (78 KiB LDS) is faster alone (1.53 vs 1.63 ms per 1000 cfg2 frames)
     // but leaves no LDS for the previous batch's DoA blocks in the pipelined chain (153 k vs 171 k frames/s)
     const long ntile = (long)F * A * ((C + CB - 1) / CB);
+    if (ntile >= (1L << 31)) return hipErrorInvalidValue;  // 32-bit tile indices in the tile kernels (readfirstlane)
     const size_t lds = sizeof(float2) * (lp_row(S) + (size_t)CB * lp_row(S));
     auto kern = k_range_fft_p<S, CB, true>;
     size_t lds_k = lds;
