@@ -299,7 +299,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MA <= 8 ? 4
   for (int x = threadIdx.x; x < nvec; x += 256) tt[x] = ttab[x];
   __syncthreads();
   const int ncell = (int)list_count(ncell_dev, ncell_host);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the wave index is wave-uniform: in an SGPR, the pass index ch and everything derived from it are scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
   const size_t plane = (size_t)S * C, fstride = (size_t)A * plane;
   const int nch = (ncell + 63) >> 6;
