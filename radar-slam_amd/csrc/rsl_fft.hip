@@ -659,7 +659,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
     t = (long)__builtin_amdgcn_readfirstlane((int)t);  // the tile index is workgroup-uniform (ntile < 2^31)
     int lt = tid;
     asm volatile("" : "+v"(lt));
-    const int row = lt >> 6, j = lt & 63;
+    const int row = __builtin_amdgcn_readfirstlane(lt >> 6), j = lt & 63;  // one wave per chirp row: row is scalar
     const int cb = (int)(t % ncb);
     const long fa = t / ncb;
     const float2* src = cube + ((size_t)fa * Ct + c0 + cb + 32 * row) * S + j;  // chirp class cb, row q = row
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(kR1kThreads) __attribute__((amdgpu_waves_per_eu(4))
     // out of the tile loop (92 registers live across it: 256 VGPRs with spills)
     int lt = tid;
     asm volatile("" : "+v"(lt));
-    const int row = lt >> 6, j = lt & 63;
+    const int row = __builtin_amdgcn_readfirstlane(lt >> 6), j = lt & 63;  // one wave per chirp row: row is scalar
     const int k1b = (lt >> 2) & 15, h = lt & 3;
     const int s_out = (h >> 1) | ((h & 1) << 1);  // the radix-4 output index lane h ends with
     float2 v[16];
