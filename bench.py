@@ -30,11 +30,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA (no 2:1 sparsity)
 DIST = False  # a torch.distributed process group is up (set in main)
-PROFILE = os.path.join(ROOT, 'profiles', 'r6o_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
+PROFILE = os.path.join(ROOT, 'profiles', 'r6p_pmc.json')  # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh)
 
 
 PROFILE_CONFIG = 'cfg2'  # the workload the committed profile was collected on
-CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r6o_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
+CFG5_PROFILE = os.path.join(ROOT, 'profiles', 'r6p_cfg5_pmc.json')  # the configs[4] frame shape (tools/profile_cfg5.sh)
 STANDALONE_RUNS = 6  # unpipelined chain runs after the timed region (kernel_ms_standalone, fft_stage_standalone)
 TRAFFIC_SOURCE = ('PMC FETCH_SIZE x 2 + WRITE_SIZE per launch from ' + os.path.relpath(PROFILE, ROOT) +
                   ' (tools/profile.sh, collected on the same kernels), scaled to this launch\'s frames')
@@ -867,7 +867,7 @@ def main():
     if extras and spec_first:
         # configs[1] first, in the process's untouched device memory: its 3 x 57 GB of spectrum buffers placed after
         # the cfg2 chain's alloc / free cycle were store-stalled (11.0 vs 9.0-9.4 ms per 1000 frames) in most
-        # placements, in untouched memory in none
+        # placements, in untouched memory less often (not never: DESIGN §5)
         spec = _spectrum_sub(ctx, dev)
     r = measure_chain(ctx, dev, A, C, Tc, F, args.steps, args.warmup, rank, world, ridge=args.ridge,
                       pipeline=bool(args.pipeline), streams=args.streams, timing=not args.no_timing)
